@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s + frame time, sponza proxy 1920x1080x256spp (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W]            (N>1: launched by torch.distributed.run)
+
+A step = one full frame of the workload: every pixel of the 1920x1080 frame traced at
+256 spp, depth 6, split into interleaved 8-row blocks over the N ranks (one MI355X each),
+followed by the RCCL all-gather of the float framebuffer.  Rank 0 prints one JSON line.
+
+value    = scene closest-hit queries (rays, counted in-kernel during warmup; the count is
+           deterministic per frame) of all ranks x K / max-over-ranks wall time of the K steps
+roofline = algorithmic bytes of rank 0's render kernel (24 B per AABB test + 36 B per
+           triangle test, scene and light BVH, + 156 B per shaded hit) per
+           launch / its average HIP-event duration, against the 8 TB/s HBM3E peak.
+cpu_baseline: the reference itself (oracle/_ref/ref_harness, built from /root/reference's
+           sources) timing Scene::render on the host cores over a bounded sample of the same
+           frame; falls back to the build's CPU restatement (oracle/) when _ref is absent.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+B_AABB, B_TRI, B_SHADE = 24, 36, 156
+
+
+def import_pkg():
+    import importlib.util
+    pkg = os.path.join(ROOT, "raytracing-hw_amd")
+    if "raytracing_hw_amd" in sys.modules:
+        return sys.modules["raytracing_hw_amd"]
+    spec = importlib.util.spec_from_file_location("raytracing_hw_amd", os.path.join(pkg, "__init__.py"),
+                                                  submodule_search_locations=[pkg])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["raytracing_hw_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_scenes_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rt_scenes", os.path.join(ROOT, "raytracing-hw_amd", "scenes.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def cpu_baseline(scene_path, width, height, spp, rows, threads):
+    """Time the reference's CPU path on a bounded sample (first `rows` rows, `spp` spp)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close")
+    sample = f"{width}x{rows} rows of the {width}x{height} frame at {spp} spp"
+    if os.path.exists(ref):
+        try:
+            out = subprocess.run([ref, "time", scene_path, str(width), str(height), str(spp), str(rows)],
+                                 env=env, capture_output=True, text=True, timeout=600, check=True).stdout
+            r = json.loads(out.strip().splitlines()[-1])
+            return {"value": r["rays"] / r["seconds"] / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                    "sample": sample + " (reference Scene::render loop, counting build)", "seconds": r["seconds"]}
+        except Exception as e:  # noqa: BLE001
+            print(f"[bench] reference CPU baseline failed: {e}", file=sys.stderr)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rtref
+    rt = import_pkg()
+    s = rt.Scene.load(scene_path, width, height, spp)
+    _, cnt, secs = rtref.Oracle().render(s.view(), spp, 0, width * rows, threads)
+    return {"value": float(cnt[0]) / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": sample + " (oracle/rt_oracle.cpp restatement)", "seconds": secs}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="sponza")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--kernel", type=int, default=0, help="0 persistent (default), 1 one-lane-per-pixel")
+    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the frame in the CPU baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    rt = import_pkg()
+    scene_dir = os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes")
+    scenes = load_scenes_module()
+    if rank == 0:
+        path = scenes.ensure_scene(args.scene, scene_dir)
+    barrier()
+    path = os.path.join(scene_dir, args.scene + ".gltf")
+    W, H, S = args.width, args.height, args.spp
+    t0 = time.time()
+    scene = rt.Scene.load(path, W, H, S)
+    scene.upload(local)
+    load_s = time.time() - t0
+    n_tris = scene.view()["tri"].shape[0]
+
+    rows = rt.shard_rows(H, rank, world, args.row_block)
+    max_rows = max(len(rt.shard_rows(H, r, world, args.row_block)) for r in range(world))
+    out = torch.zeros(max_rows * W * 3, dtype=torch.float32, device="cuda")
+    gathered = torch.empty(world * max_rows * W * 3, dtype=torch.float32, device="cuda") if world > 1 else None
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(count=False):
+        st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
+                                 count=count, kernel=args.kernel, stats=True)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+        return st
+
+    # warmup; the first one counts rays / tests (deterministic per frame, so valid for every step)
+    counts = None
+    for w in range(max(args.warmup, 1)):
+        st = step(count=(w == 0))
+        if w == 0:
+            counts = st
+    torch.cuda.synchronize()
+
+    kernel_ms = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        kernel_ms.append(st["render_ms"])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    keys = ["rays", "aabb_tests", "tri_tests", "light_queries", "light_aabb_tests", "light_tri_tests", "shading_hits"]
+    local_counts = torch.tensor([counts[k] for k in keys], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(local_counts, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    total = dict(zip(keys, local_counts.tolist()))
+    elapsed = float(t.item())
+
+    if rank == 0:
+        rays_per_frame = total["rays"]
+        value = rays_per_frame * args.steps / elapsed / 1e6
+        # rank 0's own kernel: algorithmic bytes per launch / average launch time
+        c0 = counts
+        bytes_launch = (B_AABB * (c0["aabb_tests"] + c0["light_aabb_tests"]) + B_TRI * (c0["tri_tests"] + c0["light_tri_tests"])
+                        + B_SHADE * c0["shading_hits"])
+        avg_s = float(np.mean(kernel_ms)) / 1e3
+        achieved = bytes_launch / avg_s / 1e9
+        line = {
+            "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: procedural sponza proxy (reference camera/materials/light, accessor-budget geometry, "
+                    "procedural RGBA8 textures; SURVEY.md App. C)",
+            "config": {"workload": f"{args.scene} proxy {W}x{H}x{S}spp depth 6, one frame per step",
+                       "scene": args.scene, "width": W, "height": H, "spp": S, "triangles": int(n_tris),
+                       "kernel": ["persistent", "pixel"][args.kernel], "parallelism": f"pixel-rows x{world}",
+                       "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
+                       "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
+                       "scene_load_s": round(load_s, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_launch": int(bytes_launch), "kernel_ms": round(avg_s * 1e3, 3)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(path, W, H, args.cpu_spp, min(args.cpu_rows, H), threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

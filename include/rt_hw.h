@@ -1,0 +1,149 @@
+/* rt_hw.h — C ABI of the MI355X path-tracing core (librt_hw_amd.so).
+ *
+ * The reference (Korinin38/raytracing-hw) has no plugin API; its hot path is reached
+ * through three C++ calls made by src/main.cpp:46-57.  Each entry point below replaces
+ * one of them (plain pointers and sizes, no C++ or torch types, never throws):
+ *
+ *   rt_scene_load_gltf   <- parse_scene_gltf            src/io/scene_parser.cpp:25-350
+ *                           + Scene::Scene (BVH build, light list)  src/core/scene.cpp:197-249
+ *   rt_render / rt_render_device
+ *                        <- Scene::render sample loop   src/core/scene.cpp:17-52
+ *                           (per-pixel float RGB sums = sample_canvas, scene.cpp:20,42)
+ *   rt_tonemap_u8        <- Scene::render frame finish  src/core/scene.cpp:54-64
+ *   rt_write_ppm         <- Canvas::write_to            src/render/canvas.h:76-89
+ *   rt_last_error        <- the reference's std::runtime_error messages (23 throw sites);
+ *                           the host wrappers re-throw them (drop-in failure behaviour).
+ *
+ * RNG convention: pixel (i,j) runs minstd_rand seeded with j*W+i
+ * (pixel 0 -> state 1) and a polar-normal cache reset at the pixel start, so output does
+ * not depend on threads, GPUs or the pixel partition.
+ *
+ * Status codes: 0 = OK, < 0 = error (message in rt_last_error(), thread-local).
+ */
+#ifndef RT_HW_H
+#define RT_HW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum rt_status {
+    RT_OK = 0,
+    RT_ERR_ARG = -1,      /* bad argument / NULL pointer */
+    RT_ERR_IO = -2,       /* file missing or unreadable */
+    RT_ERR_FORMAT = -3,   /* glTF / image content not supported (reference throws the same) */
+    RT_ERR_DEVICE = -4,   /* HIP runtime error or no device */
+    RT_ERR_LIMIT = -5     /* scene exceeds a device limit (e.g. BVH deeper than the stack) */
+};
+
+typedef struct rt_scene rt_scene; /* opaque: host arrays + lazily uploaded device copies */
+
+/* Read-only view of the flattened scene (the layout the kernels read from HBM).
+ * Triangles and BVH nodes are in the reference's post-build order (bvh.cpp:166 reorders
+ * `objects` in place), so object ids equal the reference's Intersection::object_id. */
+typedef struct {
+    int32_t width, height, samples, ray_depth; /* canvas, spp (scene_parser.cpp:16-22)   */
+    float max_distance;                        /* camera zfar or 1e9 (scene_parser.cpp:119) */
+    float cam_pos[3];                          /* camera.h position_                        */
+    float cam_axes[9];                         /* right, up, forward (camera.h axes_)       */
+    float cam_fov[2];                          /* fov_x, fov_y radians                      */
+    float tan_half_fov[2];                     /* tanf(fov/2) as camera.cpp:51-52 computes  */
+    uint32_t n_tris;
+    const float *tri;       /* n_tris x 12: v0.xyz, U.xyz, V.xyz, geometric normal.xyz       */
+    const float *tri_attr;  /* n_tris x 16: normal[3].xyz, texcoord[3].xy, mesh_id (int bits) */
+    const float *tri_tan;   /* n_tris x 12: tangent[3].xyzw                                   */
+    uint32_t n_nodes;
+    const float *node;      /* n_nodes x 8: aabb min.xyz, max.xyz, a, b (int bits):
+                               internal: a = left child (right = left+1), b = split_dim
+                               leaf:     a = first primitive, b = 3 | count << 2           */
+    uint32_t bvh_depth;     /* max root-to-leaf depth (root = 0)                            */
+    uint32_t n_lights;
+    const float *light;     /* n_lights x 16: v0.xyz, U.xyz, V.xyz, geo normal.xyz, area, 0,0,0
+                               (ManyLightsDistribution objects, light-BVH order)          */
+    uint32_t n_light_nodes;
+    const float *light_node; /* same format as node */
+    uint32_t light_bvh_depth;
+    uint32_t n_meshes;
+    const float *mesh_f;     /* n_meshes x 12: base_color.xyz, emission.xyz, metallic,
+                                roughness2, alpha, ior, 0, 0                               */
+    const int32_t *mesh_tex; /* n_meshes x 4: base_color_i, normal_i, metallic_roughness_i,
+                                emission_i (-1 = none)                                     */
+    const double *mesh_normal_transform; /* n_meshes x 16 (column-major matrix4d)          */
+    uint32_t n_textures;
+    const uint32_t *tex_info; /* n_textures x 4: texel offset, width, height, channels     */
+    const uint8_t *texels;    /* RGBA8, all textures concatenated                          */
+    uint64_t n_texel_bytes;
+} rt_scene_view;
+
+typedef struct {
+    int32_t spp;          /* samples per pixel (0 = the scene's)                         */
+    int32_t rank, world;  /* pixel-row partition: rows whose (row / row_block) % world == rank */
+    int32_t row_block;    /* rows per interleave block (default 8)                       */
+    int32_t count;        /* 1 = accumulate ray / AABB / triangle test counters          */
+    int32_t kernel;       /* 0 = default kernel, 1 = reference one-thread-per-pixel kernel */
+    int32_t reserved[2];
+} rt_params;
+
+typedef struct {
+    uint64_t pixels;        /* pixels rendered by this call                               */
+    uint64_t samples;       /* pixels x spp                                               */
+    uint64_t rays;          /* scene closest-hit queries (calls of BVH::intersect)         */
+    uint64_t aabb_tests;    /* AABB::intersect calls inside those queries                 */
+    uint64_t tri_tests;     /* Primitive::intersect calls inside those queries            */
+    uint64_t light_queries; /* BVH::intersectAll calls (light pdf)                        */
+    uint64_t light_aabb_tests;
+    uint64_t light_tri_tests;
+    uint64_t shading_hits;  /* scene hits that were shaded (texture / attribute fetches)  */
+    double render_ms;       /* device time of the render kernel(s), HIP events            */
+} rt_stats;
+
+/* --- scene ------------------------------------------------------------------------ */
+int rt_scene_load_gltf(const char *path, int32_t width, int32_t height, int32_t samples, rt_scene **out);
+/* Builds a scene from already-flattened arrays (same layout as rt_scene_view; copied).
+ * This is the seam for a host that keeps its own loader: e.g. the reference's parsed and
+ * BVH-built `Scene` (scene.h:14-38) flattened field by field. */
+int rt_scene_from_view(const rt_scene_view *view, rt_scene **out);
+int rt_scene_get_view(const rt_scene *scene, rt_scene_view *view);
+void rt_scene_free(rt_scene *scene);
+
+/* --- render ----------------------------------------------------------------------- */
+/* Copies the scene to `device` (once; later calls reuse it). */
+int rt_scene_upload(rt_scene *scene, int32_t device);
+/* Number of pixels a (rank, world, row_block) shard owns, and their row-major order:
+ * rows_out (may be NULL) receives the owned row indices, ascending. */
+int64_t rt_shard_rows(int32_t height, int32_t rank, int32_t world, int32_t row_block, int32_t *rows_out);
+/* Renders the shard into host memory: out_sum[k*W*3 + i*3 + c] for the k-th owned row. */
+int rt_render(rt_scene *scene, const rt_params *params, float *out_sum, rt_stats *stats);
+/* Same into device memory (d_out_sum on the scene's device, same layout) on HIP stream
+ * `stream` (NULL = default stream); returns after the launch (asynchronous) unless
+ * stats != NULL, in which case it waits and fills the counters and kernel time. */
+int rt_render_device(rt_scene *scene, const rt_params *params, float *d_out_sum, void *stream, rt_stats *stats);
+
+/* Closest hit + light pdf for n explicit rays (BVH::intersect bvh.cpp:239-243 and
+ * ManyLightsDistribution::pdf random.cpp:179-188; origin/dir as given to Ray::Ray, which
+ * normalises dir).  Host arrays: org/dir n x 3; out_f n x 4 (t, u, v, light_pdf);
+ * out_i n x 6 (hit, object id or -1, AABB tests, triangle tests, light AABB tests,
+ * light triangle tests). */
+int rt_intersect_rays(rt_scene *scene, int64_t n, const float *org, const float *dir, float *out_f, int64_t *out_i);
+
+/* --- frame finish / output (host) ---------------------------------------------------- */
+/* mean -> ACES -> powf(1/2.2) -> roundf(clamp(v*255)) per scene.cpp:54-64, vector.h:222-233, :400-407 */
+int rt_tonemap_u8(const float *sum, int32_t width, int32_t height, int32_t spp, uint8_t *rgb_out);
+/* "P6\n{W} {H}\n255\n" + raw RGB (canvas.h:76-89) */
+int rt_write_ppm(const char *path, const uint8_t *rgb, int32_t width, int32_t height);
+
+/* --- misc --------------------------------------------------------------------------- */
+const char *rt_last_error(void);
+int32_t rt_abi_version(void);
+int32_t rt_device_count(void);
+int rt_device_synchronize(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HW_H */

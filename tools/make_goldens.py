@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/ from the REFERENCE ITSELF.
+
+Runs only in the build container (needs /root/reference and oracle/_ref built by
+`make -C oracle ref`).  Every expected value below is produced by the reference's own
+compiled sources (oracle/ref_harness.cpp linked against /root/reference/src objects);
+nothing here is computed by this build's code.
+
+    python tools/make_goldens.py            # all fixtures
+Outputs (tests/golden/):
+    scenes/<name>/...                 the synthesized input scenes (raytracing-hw_amd/scenes.py)
+    <name>_dump.rtd                   reference post-BVH scene arrays (ref_harness dump)
+    <name>_sums_<W>x<H>x<S>.rtd       per-pixel float sums, per-pixel RNG reset (ref_harness sums)
+    <name>_rays.rtd                   closest-hit / light-pdf known answers (ref_harness rays)
+    cornell_samplers.rtd              SceneDistribution sample/pdf + RNG sequences
+    cornell_512x512x64_rowhash.rtd    BASELINE configs[1] full-size frame as per-row hashes
+"""
+import hashlib
+import importlib.util
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import rtdump  # noqa: E402
+
+spec = importlib.util.spec_from_file_location("rt_scenes", os.path.join(ROOT, "raytracing-hw_amd", "scenes.py"))
+scenes = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(scenes)
+
+SCENES = ["cornell", "cornell_blob", "practice6_1", "sponza_mini"]
+SUMS = {  # scene -> (W, H, spp) list
+    "cornell": [(64, 64, 8), (33, 17, 3)],
+    "cornell_blob": [(48, 48, 4)],
+    "practice6_1": [(256, 256, 4)],          # BASELINE.json configs[0] (C1), full size
+    "sponza_mini": [(64, 36, 4)],
+}
+RAYS = {"cornell": 3000, "cornell_blob": 2000, "practice6_1": 1500, "sponza_mini": 2000}
+
+
+def harness(*args):
+    out = subprocess.run([HARNESS, *map(str, args)], check=True, capture_output=True, text=True).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def compact_dump(src, dst):
+    """Keep only the fields the tests read (drops all-zero tangent / texcoord blocks)."""
+    d = rtdump.load(src)
+    keep = {}
+    for k, v in d.items():
+        if k.endswith("_aabb") and k.startswith(("obj_", "light_")):
+            continue  # per-primitive boxes are re-derived, not needed
+        if (k.endswith("tangent") or k.endswith("texcoord")) and not np.any(v):
+            continue
+        keep[k] = v
+    rtdump.save(dst, keep)
+
+
+def row_hash(sums):
+    """FNV-1a 64 of each row's float32 bit patterns (a checksum of checksums)."""
+    h = np.full(sums.shape[0], 1469598103934665603, np.uint64)
+    b = np.ascontiguousarray(sums).view(np.uint8).reshape(sums.shape[0], -1)
+    with np.errstate(over="ignore"):
+        for k in range(b.shape[1]):
+            h = (h ^ b[:, k].astype(np.uint64)) * np.uint64(1099511628211)
+    return h
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    os.makedirs(GOLD, exist_ok=True)
+    meta = {}
+    for name in SCENES:
+        sdir = os.path.join(GOLD, "scenes", name)
+        if os.path.isdir(sdir):
+            shutil.rmtree(sdir)
+        gltf = scenes.SCENES[name](sdir)
+        raw = os.path.join("/tmp", f"{name}_dump_full.rtd")
+        meta[name] = {"dump": harness("dump", gltf, 64, 64, raw)}
+        compact_dump(raw, os.path.join(GOLD, f"{name}_dump.rtd"))
+        for (w, h, s) in SUMS[name]:
+            out = os.path.join(GOLD, f"{name}_sums_{w}x{h}x{s}.rtd")
+            meta[name][f"sums_{w}x{h}x{s}"] = harness("sums", gltf, w, h, s, out, 8)
+        meta[name]["rays"] = harness("rays", gltf, 64, 64, RAYS[name], os.path.join(GOLD, f"{name}_rays.rtd"))
+    cornell = os.path.join(GOLD, "scenes", "cornell", "cornell.gltf")
+    meta["cornell"]["samplers"] = harness("samplers", cornell, 64, 64, 2000, os.path.join(GOLD, "cornell_samplers.rtd"))
+    # BASELINE.json configs[1] (C2): cornell 512x512x64 -- kept as per-row hashes + 8 full rows
+    full = "/tmp/cornell_512x512x64.rtd"
+    meta["cornell"]["sums_512x512x64"] = harness("sums", cornell, 512, 512, 64, full, 8)
+    s = rtdump.load(full)["sums"]
+    rows = np.arange(0, 512, 64)
+    rtdump.save(os.path.join(GOLD, "cornell_512x512x64_rowhash.rtd"),
+                {"row_fnv1a": row_hash(s), "rows": rows.astype(np.int32), "row_sums": s[rows],
+                 "counters": rtdump.load(full)["counters"]})
+    with open(os.path.join(GOLD, "golden_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1)[:2000])
+
+
+if __name__ == "__main__":
+    main()
