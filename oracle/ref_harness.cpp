@@ -216,12 +216,14 @@ static int mode_rays(int argc, char **argv) {
     for (auto &p : s.objects) has_lights |= p.emissive();
     std::unique_ptr<rng::ManyLightsDistribution> ml;
     if (has_lights) ml = std::make_unique<rng::ManyLightsDistribution>(s.objects);
-    auto record = [&](const Ray &r) {
+    // records the ray exactly as handed to Ray::Ray (origin, un-normalised direction)
+    auto record = [&](vector3f o, vector3f dd) {
+        Ray r(o, dd);
         reset_counters();
         t_mode = 0;
         Intersection it = s.bvh.intersect(s.objects, r);
         Counters c = total_counters();
-        for (int k = 0; k < 3; ++k) { org.push_back(r.origin[k]); dir.push_back(r.direction[k]); }
+        for (int k = 0; k < 3; ++k) { org.push_back(o[k]); dir.push_back(dd[k]); }
         hit.push_back(it.successful ? 1 : 0);
         obj.push_back(it.successful ? (int64_t)it.object_id : -1);
         t.push_back(it.successful ? it.distance : 0.f);
@@ -240,15 +242,20 @@ static int mode_rays(int argc, char **argv) {
         return it;
     };
     for (int k = 0; k < n; ++k) {
-        vector2i pp{(int)(g() % (uint64_t)W), (int)(g() % (uint64_t)H)};
-        vector2f po{U01(g) - 0.5f, U01(g) - 0.5f};
-        Ray r = s.camera->cast_in_pixel(pp, po);
-        Intersection it = record(r);
+        // camera-like ray: same construction as Camera::cast_in_pixel (camera.cpp:49-62)
+        vector2f tt{(U01(g) * 2.f - 1.f) * std::tan(s.camera->get_fov().x / 2),
+                    (U01(g) * 2.f - 1.f) * std::tan(s.camera->get_fov().y / 2)};
+        vector3f d0{};
+        d0 = d0 + tt.x * s.camera->get_axis(0);
+        d0 = d0 + tt.y * s.camera->get_axis(1);
+        d0 = d0 + 1.f * s.camera->get_axis(2);
+        vector3f o0 = s.camera->get_position();
+        Intersection it = record(o0, d0);
         if (it.successful) {
+            Ray r(o0, d0);
             vector3f pos = r.origin + r.direction * it.distance;
             vector3f d{U01(g) * 2.f - 1.f, U01(g) * 2.f - 1.f, U01(g) * 2.f - 1.f};
-            Ray r2(pos + d * 1e-4f, d);
-            record(r2);
+            record(pos + d * 1e-4f, d);
         }
     }
     RtDump d(argv[6]);
