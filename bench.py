@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--kernel", type=int, default=0, help="0 persistent (default), 1 one-lane-per-pixel")
+    ap.add_argument("--kernel", type=int, default=0, help="0 wavefront (default), 1 one lane per pixel, 2 persistent per pixel, 3 wave megakernel")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the frame in the CPU baseline sample")
     ap.add_argument("--cpu-spp", type=int, default=1)
@@ -119,17 +119,17 @@ def main():
     load_s = time.time() - t0
     n_tris = scene.view()["tri"].shape[0]
 
-    rows = rt.shard_rows(H, rank, world, args.row_block)
-    max_rows = max(len(rt.shard_rows(H, r, world, args.row_block)) for r in range(world))
+    import importlib
+    rtdist = importlib.import_module("raytracing_hw_amd.dist")
+    max_rows = rtdist.max_shard_rows(H, world, args.row_block)
     out = torch.zeros(max_rows * W * 3, dtype=torch.float32, device="cuda")
-    gathered = torch.empty(world * max_rows * W * 3, dtype=torch.float32, device="cuda") if world > 1 else None
+    frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(count=False):
         st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
                                  count=count, kernel=args.kernel, stats=True)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+        rtdist.gather_frame(out, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
         return st
 
     # warmup; the first one counts rays / tests (deterministic per frame, so valid for every step)
@@ -185,7 +185,7 @@ def main():
                     "procedural RGBA8 textures; SURVEY.md App. C)",
             "config": {"workload": f"{args.scene} proxy {W}x{H}x{S}spp depth 6, one frame per step",
                        "scene": args.scene, "width": W, "height": H, "spp": S, "triangles": int(n_tris),
-                       "kernel": ["persistent", "pixel"][args.kernel], "parallelism": f"pixel-rows x{world}",
+                       "kernel": ["wavefront", "pixel", "persistent-pixel", "wave"][args.kernel], "parallelism": f"pixel-rows x{world}",
                        "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
                        "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 3)},

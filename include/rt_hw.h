@@ -85,7 +85,7 @@ typedef struct {
     int32_t rank, world;  /* pixel-row partition: rows whose (row / row_block) % world == rank */
     int32_t row_block;    /* rows per interleave block (default 8)                       */
     int32_t count;        /* 1 = accumulate ray / AABB / triangle test counters          */
-    int32_t kernel;       /* 0 = default kernel, 1 = reference one-thread-per-pixel kernel */
+    int32_t kernel;       /* 0 = wavefront (default), 1 = one lane per pixel, 2 = persistent per-pixel, 3 = wave megakernel */
     int32_t reserved[2];
 } rt_params;
 

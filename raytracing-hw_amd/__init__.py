@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librt_hw_amd.so")
+# RT_LIB may point at the index-checked debug build (make -C raytracing-hw_amd debug)
+LIB_PATH = os.environ.get("RT_LIB") or os.path.join(_HERE, "librt_hw_amd.so")
 REPO_ROOT = os.path.dirname(_HERE)
 
 _c_f = ctypes.POINTER(ctypes.c_float)

@@ -15,6 +15,8 @@
 #include <vector>
 
 #include "rt_path.h"
+#include "rt_wave.h"
+#include "rt_wavefront.h"
 #include "rt_scene.h"
 
 using rtd::Counters;
@@ -27,6 +29,14 @@ struct rt_device_scene {
     unsigned long long *counters = nullptr;  // 6 x u64
     unsigned int *queue = nullptr;           // persistent kernel work counter
     int cu_count = 0;
+    // wavefront path state (allocated on first use, grown on demand)
+    void *wf_buf = nullptr;
+    long long wf_cap = 0;
+    int wf_D = 0;
+    rtd::WfState wf{};
+    int *wf_queue[2] = {nullptr, nullptr};
+    unsigned *wf_count = nullptr;  // [2]
+    unsigned *wf_host_count = nullptr;  // pinned
 };
 
 #define HIP_TRY(expr)                                                                          \
@@ -37,16 +47,8 @@ struct rt_device_scene {
     } while (0)
 
 // ------------------------------------------------------------------------ kernels
-struct ShardGeom {
-    int width, rank, world, row_block;
-    long long n_pixels;
-};
-
-__device__ __forceinline__ int shard_row(const ShardGeom &g, int k) {
-    // k-th owned row: rows whose (row / row_block) % world == rank, ascending
-    const int blk = k / g.row_block;
-    return (blk * g.world + g.rank) * g.row_block + (k % g.row_block);
-}
+using rtd::ShardGeom;
+using rtd::shard_row;
 
 template <bool COUNT>
 __device__ __forceinline__ void flush_counters(const Counters &c, unsigned long long *out) {
@@ -100,6 +102,147 @@ __global__ void __launch_bounds__(256) rt_persistent_kernel(DevScene sc, ShardGe
         }
     }
     flush_counters<COUNT>(cnt, counters);
+}
+
+// Wave-synchronous persistent kernel (rt_wave.h): lanes run a flat
+// IDLE -> TRAV -> SHADE state machine so a wave never waits for a whole path or pixel.
+// Exit: the per-launch queue is monotonic, so once a refill reaches n_pixels the wave
+// stops asking; the loop ends when no lane holds a pixel.
+template <bool COUNT>
+__global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, int spp, float *out,
+                                                       unsigned long long *counters, unsigned int *queue) {
+    const int lane = threadIdx.x & 63;
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    rtd::Lane L;
+    rtd::lane_init(L);
+    bool exhausted = false;
+    for (;;) {
+        // (A) refill: one atomic per wave for all lanes without a pixel
+        if (!exhausted) {
+            const bool need = L.pix < 0;
+            const unsigned long long m = __ballot(need);
+            if (m) {
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                const unsigned cntm = (unsigned)__popcll(m);
+                unsigned base = 0;
+                if (lane == leader) base = atomicAdd(queue, cntm);
+                base = __shfl(base, leader, 64);
+                if (need) {
+                    const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
+                    if (p < g.n_pixels) rtd::lane_assign(L, sc, g, p);
+                }
+                if ((long long)base + cntm >= g.n_pixels) exhausted = true;
+            }
+        }
+        if (!__any(L.pix >= 0)) break;
+        // (B) IDLE lanes start their next sample
+        if (L.pix >= 0 && L.state == rtd::L_IDLE) rtd::lane_start_sample<COUNT>(L, sc, g, cnt);
+        // (C) traversal: all traversing lanes step together
+        bool trav = L.state == rtd::L_TRAV;
+        while (__any(trav)) {
+            if (trav) trav = rtd::trav_step<COUNT>(sc, L.r, L.t, L.stk, cnt);
+        }
+        if (L.state == rtd::L_TRAV) L.state = rtd::L_SHADE;
+        // (D) shade, bounce or end the path
+        if (L.state == rtd::L_SHADE) rtd::lane_shade<COUNT>(L, sc, spp, out, cnt);
+    }
+    flush_counters<COUNT>(cnt, counters);
+}
+
+// ------------------------------------------------------------------------ wavefront
+// (rt_wavefront.h) init -> { extend ; shade } until every slot has finished its samples.
+__global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int *queue,
+                                                       unsigned *count) {
+    for (long long base = (long long)blockIdx.x * blockDim.x; base < st.n; base += (long long)gridDim.x * blockDim.x) {
+        const long long i = base + threadIdx.x;
+        const bool valid = i < st.n;
+        if (valid) {
+            const int k = (int)(i / g.width), px = (int)(i % g.width), py = shard_row(g, k);
+            const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;  // scene.cpp:34
+            rtd::Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
+            int power = 0;
+            const rtd::Ray r = rtd::start_sample(sc, g, i, rng, power);
+            rtd::store_ray(st, i, r);
+            st.sx[i] = st.sy[i] = st.sz[i] = 0.f;
+            st.rng_x[i] = rng.x;
+            st.rng_saved[i] = rng.saved;
+            st.meta[i] = rtd::meta_pack(0, power, 0, rng.saved_avail);
+        }
+        rtd::queue_push(valid, (int)i, queue, count);
+    }
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfState st, const int *queue,
+                                                         const unsigned *count, unsigned long long *counters) {
+    const unsigned n = *count;
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    uint2 stk[rtd::kStack];
+    for (unsigned q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const int i = queue[q];
+        const rtd::Ray r = rtd::load_ray(st, i);
+        rtd::Trav t;
+        if (rtd::trav_begin<COUNT>(sc, r, t, cnt))
+            while (rtd::trav_step<COUNT>(sc, r, t, stk, cnt)) {
+            }
+        st.hprim[i] = t.best.prim;
+        st.ht[i] = t.best.t;
+        st.hu[i] = t.best.u;
+        st.hv[i] = t.best.v;
+    }
+    rtd::counters_flush<COUNT>(cnt, counters);
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp,
+                                                        const int *qin, const unsigned *cin, int *qout, unsigned *cout,
+                                                        float *out, unsigned long long *counters) {
+    const unsigned n = *cin;
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    for (unsigned base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const unsigned q = base + threadIdx.x;
+        const bool valid = q < n;
+        const int i = valid ? qin[q] : 0;
+        bool next = false;
+        if (valid) {
+            rtd::Ray r = rtd::load_ray(st, i);
+            const uint32_t meta = st.meta[i];
+            int s = (int)(meta & 0xfffffu), power = (int)((meta >> 20) & 15u), nv = (int)((meta >> 24) & 15u);
+            rtd::Rng rng{st.rng_x[i], (meta >> 28) & 1u, st.rng_saved[i]};
+            rtd::SoARec P{st.rec, st.n, (long long)i, st.D};
+            const rtd::Hit h{st.ht[i], st.hu[i], st.hv[i], st.hprim[i]};
+            // scene.cpp:85-154 for this vertex; the recursion goes on while calls remain
+            if (h.prim >= 0 && h.t < sc.max_distance && rtd::shade_hit<COUNT>(sc, r, h, rng, cnt, P, nv)) {
+                if (power > 0) {
+                    power -= 1;
+                    next = true;
+                }
+            }
+            if (!next) {
+                // path over: fold, accumulate (scene.cpp:41-42), next sample or pixel done
+                const rtv::V3 c = rtd::fold_path(P, nv);
+                const float ax = st.sx[i] + c.x, ay = st.sy[i] + c.y, az = st.sz[i] + c.z;
+                st.sx[i] = ax;
+                st.sy[i] = ay;
+                st.sz[i] = az;
+                if (++s == spp) {
+                    out[3 * (long long)i + 0] = ax;
+                    out[3 * (long long)i + 1] = ay;
+                    out[3 * (long long)i + 2] = az;
+                } else {
+                    r = rtd::start_sample(sc, g, i, rng, power);
+                    nv = 0;
+                    next = true;
+                }
+            }
+            if (next) rtd::store_ray(st, i, r);
+            st.meta[i] = rtd::meta_pack(s, power, nv, rng.saved_avail);
+            st.rng_x[i] = rng.x;
+            st.rng_saved[i] = rng.saved;
+        }
+        rtd::queue_push(next, i, qout, cout);
+    }
+    rtd::counters_flush<COUNT>(cnt, counters);
 }
 
 // Ray-level entry: BVH::intersect + ManyLightsDistribution::pdf for explicit rays.
@@ -183,6 +326,9 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.tex_info = (const uint4 *)(b + o_ti);
     ds.texels = (const uint32_t *)(b + o_tx);
     ds.n_lights = (int)(s->light.size() / 16);
+    ds.n_tris = (int)(s->tri.size() / 12);
+    ds.n_nodes = (int)(s->node.size() / 8);
+    ds.n_meshes = (int)(s->mesh_f.size() / 12);
     ds.ray_depth = s->ray_depth;
     ds.max_distance = s->max_distance;
     ds.width = s->width;
@@ -194,11 +340,97 @@ int ensure_device_scene(rt_scene *s, int device) {
     return RT_OK;
 }
 
+// Wavefront workspace: SoA path state for `n` slots with `D` vertex records each.
+int ensure_wf(rt_device_scene *d, long long n, int D) {
+    if (d->wf_buf && d->wf_cap >= n && d->wf_D == D) return RT_OK;
+    if (d->wf_buf) (void)hipFree(d->wf_buf);
+    if (d->wf_count) (void)hipFree(d->wf_count);
+    if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
+    d->wf_buf = nullptr;
+    d->wf_count = nullptr;
+    d->wf_host_count = nullptr;
+    const long long cap = ((n + 255) / 256) * 256;
+    const int planes_f = 6 + 3 + 1 + 3 + 9 * D;   // ray, hit t/u/v, rng_saved, sums, records
+    const int planes_i = 1 + 1 + 1 + 2;           // hprim, rng_x, meta, queues
+    const size_t bytes = (size_t)cap * 4 * (size_t)(planes_f + planes_i);
+    HIP_TRY(hipMalloc(&d->wf_buf, bytes));
+    HIP_TRY(hipMalloc((void **)&d->wf_count, 64));
+    HIP_TRY(hipHostMalloc((void **)&d->wf_host_count, 64, hipHostMallocDefault));
+    float *f = (float *)d->wf_buf;
+    auto take = [&](void) { float *p = f; f += cap; return p; };
+    rtd::WfState &w = d->wf;
+    w.n = n;
+    w.D = D;
+    w.ox = take(); w.oy = take(); w.oz = take(); w.dx = take(); w.dy = take(); w.dz = take();
+    w.ht = take(); w.hu = take(); w.hv = take();
+    w.rng_saved = take();
+    w.sx = take(); w.sy = take(); w.sz = take();
+    w.rec = f;
+    f += (size_t)cap * 9 * D;
+    w.hprim = (int *)take();
+    w.rng_x = (uint32_t *)take();
+    w.meta = (uint32_t *)take();
+    d->wf_queue[0] = (int *)take();
+    d->wf_queue[1] = (int *)take();
+    d->wf_cap = cap;
+    d->wf_D = D;
+    return RT_OK;
+}
+
+template <class K>
+unsigned persistent_blocks(rt_device_scene *d, K kernel, long long work) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    long long need = (work + 255) / 256;
+    long long b = std::min<long long>(need, (long long)d->cu_count * per_cu);
+    return (unsigned)std::max<long long>(b, 1);
+}
+
+int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth, float *d_out, hipStream_t stream,
+                     bool count) {
+    if (depth < 1 || depth > 15) return rt_fail(RT_ERR_LIMIT, "wavefront path: ray_depth must be in [1, 15]");
+    if (spp >= (1 << 20)) return rt_fail(RT_ERR_LIMIT, "wavefront path: spp must be < 2^20");
+    int rc = ensure_wf(d, g.n_pixels, depth);
+    if (rc) return rc;
+    rtd::WfState w = d->wf;
+    w.n = g.n_pixels;
+    HIP_TRY(hipMemsetAsync(d->wf_count, 0, 8, stream));
+    const unsigned init_blocks = (unsigned)std::min<long long>((g.n_pixels + 255) / 256, (long long)d->cu_count * 8);
+    hipLaunchKernelGGL(wf_init_kernel, dim3(init_blocks), dim3(256), 0, stream, d->ds, g, w, d->wf_queue[0], &d->wf_count[0]);
+    HIP_TRY(hipGetLastError());
+    const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, g.n_pixels)
+                                      : persistent_blocks(d, wf_extend_kernel<false>, g.n_pixels);
+    const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true>, g.n_pixels)
+                                     : persistent_blocks(d, wf_shade_kernel<false>, g.n_pixels);
+    const long long max_iter = (long long)spp * depth + 16;
+    int cur = 0;
+    for (long long it = 0;; ++it) {
+        if (it > max_iter) return rt_fail(RT_ERR_DEVICE, "wavefront path did not drain (internal error)");
+        HIP_TRY(hipMemsetAsync(&d->wf_count[1 - cur], 0, 4, stream));
+        if (count) {
+            hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
+            hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
+        } else {
+            hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
+            hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
+        }
+        HIP_TRY(hipGetLastError());
+        cur = 1 - cur;
+        if ((it & 7) == 7) {
+            HIP_TRY(hipMemcpyAsync(d->wf_host_count, &d->wf_count[cur], 4, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            if (*d->wf_host_count == 0) break;
+        }
+    }
+    return RT_OK;
+}
+
 int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt_stats *st) {
     if (!s || !p || !d_out) return rt_fail(RT_ERR_ARG, "rt_render: NULL argument");
     if (!s->dev) return rt_fail(RT_ERR_ARG, "rt_render: scene not uploaded");
     const int world = p->world > 0 ? p->world : 1, rank = p->rank, rb = p->row_block > 0 ? p->row_block : 8;
     const int spp = p->spp > 0 ? p->spp : s->samples;
+    if (spp < 1) return rt_fail(RT_ERR_ARG, "rt_render: samples per pixel must be >= 1");
     const int64_t rows = rt_shard_rows_impl(s->height, rank, world, rb, nullptr);
     if (rows < 0) return RT_ERR_ARG;
     ShardGeom g{s->width, rank, world, rb, (long long)rows * s->width};
@@ -218,14 +450,27 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const unsigned blocks = (unsigned)((g.n_pixels + 255) / 256);
             if (count) hipLaunchKernelGGL(rt_pixels_kernel<true>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters);
             else hipLaunchKernelGGL(rt_pixels_kernel<false>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters);
-        } else {
-            // persistent grid: enough waves to fill every SIMD a few times over
+        } else if (p->kernel == 2) {
             long long waves = (g.n_pixels + 63) / 64;
-            long long want = (long long)d->cu_count * 16;  // 16 waves per CU = 4 blocks of 256
+            long long want = (long long)d->cu_count * 16;
             unsigned blocks = (unsigned)((std::min(waves, want) + 3) / 4);
             if (blocks == 0) blocks = 1;
             if (count) hipLaunchKernelGGL(rt_persistent_kernel<true>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
             else hipLaunchKernelGGL(rt_persistent_kernel<false>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
+        } else if (p->kernel == 0) {
+            int rc = launch_wavefront(d, g, spp, s->ray_depth, d_out, stream, count);
+            if (rc) return rc;
+        } else {
+            // persistent wave kernel: exactly the resident blocks (occupancy query), capped by the work
+            int per_cu = 0;
+            if (count) HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_wave_kernel<true>, 256, 0));
+            else HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rt_wave_kernel<false>, 256, 0));
+            if (per_cu < 1) per_cu = 1;
+            long long need = (g.n_pixels + 255) / 256;
+            unsigned blocks = (unsigned)std::min<long long>(need, (long long)d->cu_count * per_cu);
+            if (blocks == 0) blocks = 1;
+            if (count) hipLaunchKernelGGL(rt_wave_kernel<true>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
+            else hipLaunchKernelGGL(rt_wave_kernel<false>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
         }
         HIP_TRY(hipGetLastError());
     }
@@ -260,6 +505,9 @@ void rt_device_scene_release(rt_scene *s) {
         if (d->buf) (void)hipFree(d->buf);
         if (d->counters) (void)hipFree(d->counters);
         if (d->queue) (void)hipFree(d->queue);
+        if (d->wf_buf) (void)hipFree(d->wf_buf);
+        if (d->wf_count) (void)hipFree(d->wf_count);
+        if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
     }
     delete d;
     s->dev = nullptr;
@@ -330,6 +578,16 @@ int rt_intersect_rays(rt_scene *s, int64_t n, const float *org, const float *dir
     if (e != hipSuccess) return rt_fail(RT_ERR_DEVICE, std::string("rt_intersect_rays: ") + hipGetErrorString(e));
     return RT_OK;
 }
+
+#if defined(RT_DEBUG_CHECKS)
+// debug builds only: first recorded index violation (code << 56 | value), 0 = none
+int rt_debug_take(unsigned long long *word) {
+    unsigned long long z = 0;
+    HIP_TRY(hipMemcpyFromSymbol(word, HIP_SYMBOL(rt_debug_word), sizeof z));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rt_debug_word), &z, sizeof z));
+    return RT_OK;
+}
+#endif
 
 int32_t rt_device_count(void) {
     int n = 0;

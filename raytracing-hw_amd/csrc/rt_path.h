@@ -29,6 +29,21 @@ using std::isnan;
 #include "rt_srgb_lut.h"
 #include "rt_vec.h"
 
+// Debug build (make DEBUG_CHECKS=1): index checks that record the first violation in
+// rt_debug_word (code << 56 | value) and clamp the index so the kernel completes.
+#if defined(RT_DEBUG_CHECKS) && defined(__HIPCC__)
+__device__ unsigned long long rt_debug_word;
+#define RT_CHECK(cond, code, val, fix)                                                                        \
+    do {                                                                                                     \
+        if (!(cond)) {                                                                                       \
+            atomicCAS(&rt_debug_word, 0ull, ((unsigned long long)(code) << 56) | ((unsigned long long)(val) & 0xffffffffffffffull)); \
+            fix;                                                                                             \
+        }                                                                                                    \
+    } while (0)
+#else
+#define RT_CHECK(cond, code, val, fix) do { } while (0)
+#endif
+
 namespace rtd {
 
 using rtv::V2;
@@ -55,6 +70,7 @@ struct DevScene {
     const uint4 *tex_info;    // texel offset, width, height, channels
     const uint32_t *texels;   // RGBA8
     int n_lights;
+    int n_tris, n_nodes, n_meshes;
     int ray_depth;
     float max_distance;
     int width, height;
@@ -462,14 +478,159 @@ __device__ __forceinline__ V3 mul_vector_d(const double *m, V3 t) {
     return V3{res[0], res[1], res[2]};
 }
 
-// ------------------------------------------------------------------------ one sample
-// Scene::intersect (scene.cpp:71-157) unrolled into a forward pass that records each
-// path vertex, followed by the backward fold c_k = e_k + ((((c_{k+1}*coeff)*mat)*cos)*alpha)
+// ------------------------------------------------------------------------ path vertices
+// Scene::intersect (scene.cpp:71-157) is recursive; the kernels run it as a forward pass
+// that records each path vertex, followed by the backward fold
+//     c_k = e_k + ((((c_{k+1} * coeff_k) * material_k) * cos_k) * alpha_k)
 // which reproduces the recursion's rounding exactly.
+struct PathRec {
+    V3 e[kMaxDepth], m[kMaxDepth];
+    float coeff[kMaxDepth], cosv[kMaxDepth], alpha[kMaxDepth];
+    __device__ __forceinline__ void set_e(int k, V3 v) { e[k] = v; }
+    __device__ __forceinline__ void set_brdf(int k, V3 mm, float c, float cs, float a) {
+        m[k] = mm;
+        coeff[k] = c;
+        cosv[k] = cs;
+        alpha[k] = a;
+    }
+    __device__ __forceinline__ V3 get_e(int k) const { return e[k]; }
+    __device__ __forceinline__ V3 get_m(int k) const { return m[k]; }
+    __device__ __forceinline__ float get_coeff(int k) const { return coeff[k]; }
+    __device__ __forceinline__ float get_cos(int k) const { return cosv[k]; }
+    __device__ __forceinline__ float get_alpha(int k) const { return alpha[k]; }
+};
+
+// The same records kept structure-of-arrays in HBM for the wavefront pipeline:
+// plane (q * D + k) holds component q of vertex k for every path slot.
+struct SoARec {
+    float *base;
+    long long n;   // slots
+    long long i;   // this slot
+    int D;         // vertex capacity
+    __device__ __forceinline__ float &at(int q, int k) const { return base[((long long)(q * D + k)) * n + i]; }
+    __device__ __forceinline__ void set_e(int k, V3 v) const { at(0, k) = v.x; at(1, k) = v.y; at(2, k) = v.z; }
+    __device__ __forceinline__ void set_brdf(int k, V3 mm, float c, float cs, float a) const {
+        at(3, k) = mm.x; at(4, k) = mm.y; at(5, k) = mm.z;
+        at(6, k) = c; at(7, k) = cs; at(8, k) = a;
+    }
+    __device__ __forceinline__ V3 get_e(int k) const { return V3{at(0, k), at(1, k), at(2, k)}; }
+    __device__ __forceinline__ V3 get_m(int k) const { return V3{at(3, k), at(4, k), at(5, k)}; }
+    __device__ __forceinline__ float get_coeff(int k) const { return at(6, k); }
+    __device__ __forceinline__ float get_cos(int k) const { return at(7, k); }
+    __device__ __forceinline__ float get_alpha(int k) const { return at(8, k); }
+};
+
+// One hit of Scene::intersect (scene.cpp:85-154): records vertex nv (its emission and, if
+// the path continues, its BRDF factors), advances nv and replaces r by the bounce ray.
+// Returns false where the recursion returns at this vertex (sample below the surface,
+// pdf <= 0 or NaN).
+template <bool COUNT, class Rec>
+__device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
+    if (COUNT) cnt.hits++;
+    int id = hit.prim;
+    RT_CHECK(id >= 0 && id < sc.n_tris, 1, id, id = 0);
+    RT_CHECK(nv >= 0 && nv < kMaxDepth - 1, 2, nv, nv = 0);
+    const float u = hit.u, v = hit.v;
+    const float4 t2 = sc.tri[3 * id + 2];
+    V3 ngeo{t2.y, t2.z, t2.w};
+    bool inside = false;
+    if (rtv::dot(r.d, ngeo) > 0) { inside = true; ngeo = rtv::neg(ngeo); }
+    const float4 a0 = sc.tri_attr[4 * id], a1 = sc.tri_attr[4 * id + 1], a2 = sc.tri_attr[4 * id + 2],
+                 a3 = sc.tri_attr[4 * id + 3];
+    int mesh = __float_as_int(a3.w);
+    RT_CHECK(mesh >= 0 && mesh < sc.n_meshes, 3, mesh, mesh = 0);
+    const float *mf = sc.mesh_f + 12 * mesh;
+    const int *mt = sc.mesh_tex + 4 * mesh;
+    const float w = 1 - u - v;
+    const V2 tc{w * a2.y + u * a2.w + v * a3.y, w * a2.z + u * a3.x + v * a3.z};
+    // Primitive::get_emission (primitive.cpp:121-129)
+    V3 emission{mf[3], mf[4], mf[5]};
+    if (mt[3] >= 0) emission = rtv::mulv(rtv::reduce(tex_sample(sc, mt[3], tc, true)), emission);
+    P.set_e(nv, emission);
+    // Primitive::get_shading_normal (primitive.cpp:86-105)
+    V3 n0{a0.x, a0.y, a0.z}, n1{a0.w, a1.x, a1.y}, n2{a1.z, a1.w, a2.x};
+    V3 lz = rtv::normal(rtv::add(rtv::add(rtv::mul(n0, w), rtv::mul(n1, u)), rtv::mul(n2, v)));
+    V3 N = lz;
+    if (mt[1] >= 0) {
+        const float4 g0 = sc.tri_tan[3 * id], g1 = sc.tri_tan[3 * id + 1], g2 = sc.tri_tan[3 * id + 2];
+        V3 t0{g0.x, g0.y, g0.z}, t1{g1.x, g1.y, g1.z}, tt2{g2.x, g2.y, g2.z};
+        V3 lx = rtv::normal(mul_vector_d(sc.mesh_nt + 16 * mesh,
+                                         rtv::normal(rtv::add(rtv::add(rtv::mul(t0, w), rtv::mul(t1, u)), rtv::mul(tt2, v)))));
+        V3 ly = rtv::mul(rtv::cross(lz, lx), g0.w);
+        V3 s = rtv::reduce(tex_sample(sc, mt[1], tc, false));
+        V3 ln = rtv::mul(rtv::addf(s, -0.5f), 2.f);
+        N = rtv::normal(rtv::add(rtv::add(rtv::mul(lx, ln.x), rtv::mul(ly, ln.y)), rtv::mul(lz, ln.z)));
+    }
+    if (inside) N = rtv::neg(N);
+    // Primitive::get_metallic_roughness (primitive.cpp:131-140)
+    float r2 = mf[7], metallic = mf[6];
+    if (mt[2] >= 0) {
+        V4 mr = tex_sample(sc, mt[2], tc, false);
+        float rr = mr.y * mr.y;
+        r2 = rr * mf[7];
+        metallic = mr.z * mf[6];
+    }
+    r2 = rtv::smax(kRoughness2Limit, r2);
+    const V3 pos = rtv::add(r.o, rtv::mul(r.d, hit.t));
+    const V3 eye = rtv::neg(r.d);
+    // SceneDistribution::sample (random.cpp:194-208)
+    V3 dir;
+    {
+        float s = (rng_uniform_m11(rng) + 1.f) * 3 * 0.5f;
+        if (!sc.n_lights) s /= 1.5f;
+        if (s <= 1.f) dir = cosine_sample(N, rng);
+        else if (s <= 2.f) dir = vndf_sample(N, eye, r2, rng);
+        else dir = light_sample(sc, pos, rng);
+    }
+    nv++;
+    if (rtv::dot(dir, N) <= 0.f) {
+        if (rtv::dot(dir, ngeo) <= 0.f) return false;
+        N = ngeo;
+    }
+    // SceneDistribution::pdf (random.cpp:210-218)
+    float pdf;
+    if (!sc.n_lights) pdf = (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
+    else pdf = (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt) + vndf_pdf(N, eye, r2, dir)) / 3;
+    if (pdf <= 0.f || isnan(pdf)) return false;
+    // BRDF of this vertex (scene.cpp:134-154): used only if the child ray hits
+    const float coeff = 1 / pdf;
+    const V3 half = rtv::normal(rtv::sub(dir, r.d));
+    const float vis = smith(r2, N, eye, dir) * (1.f / (4 * fabsf(rtv::dot(N, r.d)) * fabsf(rtv::dot(N, dir))));
+    const float spec = ggx(r2, N, half) * vis;
+    const float VdotH = fabsf(rtv::dot(eye, half));
+    V3 base{mf[0], mf[1], mf[2]};
+    if (mt[0] >= 0) base = rtv::mulv(rtv::reduce(tex_sample(sc, mt[0], tc, true)), base);
+    const float p5 = rtm::pow5_glibc(1.f - VdotH);
+    const V3 fres{base.x + (1.f - base.x) * p5, base.y + (1.f - base.y) * p5, base.z + (1.f - base.z) * p5};
+    const V3 metal = rtv::mul(fres, spec);
+    const V3 diffuse = rtv::mul(base, kInvPiF);
+    const float dsc = 0.04f + (1.f - 0.04f) * p5;
+    const V3 dielectric = rtv::add(rtv::mul(diffuse, 1 - dsc), rtv::mul(rtv::mul(V3{1.f, 1.f, 1.f}, spec), dsc));
+    P.set_brdf(nv - 1, rtv::add(rtv::mul(dielectric, 1 - metallic), rtv::mul(metal, metallic)), coeff,
+               rtv::dot(dir, N), mf[8]);
+    r = make_ray(rtv::add(pos, rtv::mul(dir, kStep)), dir);
+    return true;
+}
+
+// Backward fold over the recorded vertices (a primary miss gives bg colour 0).
+template <class Rec>
+__device__ __forceinline__ V3 fold_path(const Rec &P, int nv) {
+    if (nv == 0) return V3{0.f, 0.f, 0.f};
+    V3 c = P.get_e(nv - 1);
+    for (int k = nv - 2; k >= 0; --k) {
+        V3 x = rtv::mul(c, P.get_coeff(k));
+        x = rtv::mulv(x, P.get_m(k));
+        x = rtv::mul(x, P.get_cos(k));
+        x = rtv::mul(x, P.get_alpha(k));
+        c = rtv::add(P.get_e(k), x);
+    }
+    return c;
+}
+
+// One sample: ray_depth traversals at most (the 7th call returns without tracing).
 template <bool COUNT>
 __device__ V3 trace_sample(const DevScene &sc, Ray r, Rng &rng, Counters &cnt) {
-    V3 e_[kMaxDepth], m_[kMaxDepth];
-    float coeff_[kMaxDepth], cos_[kMaxDepth], alpha_[kMaxDepth];
+    PathRec P;
     int nv = 0;
     int power = sc.ray_depth;
     while (power > 0) {
@@ -477,99 +638,9 @@ __device__ V3 trace_sample(const DevScene &sc, Ray r, Rng &rng, Counters &cnt) {
         Hit hit;
         bool ok = closest_hit<COUNT>(sc, r, hit, cnt);
         if (!(ok && hit.t < sc.max_distance)) break;   // miss: bg colour 0, unsuccessful
-        if (COUNT) cnt.hits++;
-        const int id = hit.prim;
-        const float u = hit.u, v = hit.v;
-        const float4 t2 = sc.tri[3 * id + 2];
-        V3 ngeo{t2.y, t2.z, t2.w};
-        bool inside = false;
-        if (rtv::dot(r.d, ngeo) > 0) { inside = true; ngeo = rtv::neg(ngeo); }
-        const float4 a0 = sc.tri_attr[4 * id], a1 = sc.tri_attr[4 * id + 1], a2 = sc.tri_attr[4 * id + 2],
-                     a3 = sc.tri_attr[4 * id + 3];
-        const int mesh = __float_as_int(a3.w);
-        const float *mf = sc.mesh_f + 12 * mesh;
-        const int *mt = sc.mesh_tex + 4 * mesh;
-        const float w = 1 - u - v;
-        const V2 tc{w * a2.y + u * a2.w + v * a3.y, w * a2.z + u * a3.x + v * a3.z};
-        // Primitive::get_emission (primitive.cpp:121-129)
-        V3 emission{mf[3], mf[4], mf[5]};
-        if (mt[3] >= 0) emission = rtv::mulv(rtv::reduce(tex_sample(sc, mt[3], tc, true)), emission);
-        e_[nv] = emission;
-        // Primitive::get_shading_normal (primitive.cpp:86-105)
-        V3 n0{a0.x, a0.y, a0.z}, n1{a0.w, a1.x, a1.y}, n2{a1.z, a1.w, a2.x};
-        V3 lz = rtv::normal(rtv::add(rtv::add(rtv::mul(n0, w), rtv::mul(n1, u)), rtv::mul(n2, v)));
-        V3 N = lz;
-        if (mt[1] >= 0) {
-            const float4 g0 = sc.tri_tan[3 * id], g1 = sc.tri_tan[3 * id + 1], g2 = sc.tri_tan[3 * id + 2];
-            V3 t0{g0.x, g0.y, g0.z}, t1{g1.x, g1.y, g1.z}, tt2{g2.x, g2.y, g2.z};
-            V3 lx = rtv::normal(mul_vector_d(sc.mesh_nt + 16 * mesh,
-                                             rtv::normal(rtv::add(rtv::add(rtv::mul(t0, w), rtv::mul(t1, u)), rtv::mul(tt2, v)))));
-            V3 ly = rtv::mul(rtv::cross(lz, lx), g0.w);
-            V3 s = rtv::reduce(tex_sample(sc, mt[1], tc, false));
-            V3 ln = rtv::mul(rtv::addf(s, -0.5f), 2.f);
-            N = rtv::normal(rtv::add(rtv::add(rtv::mul(lx, ln.x), rtv::mul(ly, ln.y)), rtv::mul(lz, ln.z)));
-        }
-        if (inside) N = rtv::neg(N);
-        // Primitive::get_metallic_roughness (primitive.cpp:131-140)
-        float r2 = mf[7], metallic = mf[6];
-        if (mt[2] >= 0) {
-            V4 mr = tex_sample(sc, mt[2], tc, false);
-            float rr = mr.y * mr.y;
-            r2 = rr * mf[7];
-            metallic = mr.z * mf[6];
-        }
-        r2 = rtv::smax(kRoughness2Limit, r2);
-        const V3 pos = rtv::add(r.o, rtv::mul(r.d, hit.t));
-        const V3 eye = rtv::neg(r.d);
-        // SceneDistribution::sample (random.cpp:194-208)
-        V3 dir;
-        {
-            float s = (rng_uniform_m11(rng) + 1.f) * 3 * 0.5f;
-            if (!sc.n_lights) s /= 1.5f;
-            if (s <= 1.f) dir = cosine_sample(N, rng);
-            else if (s <= 2.f) dir = vndf_sample(N, eye, r2, rng);
-            else dir = light_sample(sc, pos, rng);
-        }
-        nv++;
-        if (rtv::dot(dir, N) <= 0.f) {
-            if (rtv::dot(dir, ngeo) <= 0.f) break;
-            N = ngeo;
-        }
-        // SceneDistribution::pdf (random.cpp:210-218)
-        float pdf;
-        if (!sc.n_lights) pdf = (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
-        else pdf = (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt) + vndf_pdf(N, eye, r2, dir)) / 3;
-        if (pdf <= 0.f || isnan(pdf)) break;
-        // BRDF of this vertex (scene.cpp:134-154): used only if the child ray hits
-        const float coeff = 1 / pdf;
-        const V3 half = rtv::normal(rtv::sub(dir, r.d));
-        const float vis = smith(r2, N, eye, dir) * (1.f / (4 * fabsf(rtv::dot(N, r.d)) * fabsf(rtv::dot(N, dir))));
-        const float spec = ggx(r2, N, half) * vis;
-        const float VdotH = fabsf(rtv::dot(eye, half));
-        V3 base{mf[0], mf[1], mf[2]};
-        if (mt[0] >= 0) base = rtv::mulv(rtv::reduce(tex_sample(sc, mt[0], tc, true)), base);
-        const float p5 = rtm::pow5_glibc(1.f - VdotH);
-        const V3 fres{base.x + (1.f - base.x) * p5, base.y + (1.f - base.y) * p5, base.z + (1.f - base.z) * p5};
-        const V3 metal = rtv::mul(fres, spec);
-        const V3 diffuse = rtv::mul(base, kInvPiF);
-        const float dsc = 0.04f + (1.f - 0.04f) * p5;
-        const V3 dielectric = rtv::add(rtv::mul(diffuse, 1 - dsc), rtv::mul(rtv::mul(V3{1.f, 1.f, 1.f}, spec), dsc));
-        m_[nv - 1] = rtv::add(rtv::mul(dielectric, 1 - metallic), rtv::mul(metal, metallic));
-        coeff_[nv - 1] = coeff;
-        cos_[nv - 1] = rtv::dot(dir, N);
-        alpha_[nv - 1] = mf[8];
-        r = make_ray(rtv::add(pos, rtv::mul(dir, kStep)), dir);
+        if (!shade_hit<COUNT>(sc, r, hit, rng, cnt, P, nv)) break;
     }
-    if (nv == 0) return V3{0.f, 0.f, 0.f};
-    V3 c = e_[nv - 1];
-    for (int k = nv - 2; k >= 0; --k) {
-        V3 x = rtv::mul(c, coeff_[k]);
-        x = rtv::mulv(x, m_[k]);
-        x = rtv::mul(x, cos_[k]);
-        x = rtv::mul(x, alpha_[k]);
-        c = rtv::add(e_[k], x);
-    }
-    return c;
+    return fold_path(P, nv);
 }
 
 // Camera::cast_in_pixel (camera.cpp:49-62)

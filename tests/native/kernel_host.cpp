@@ -3,7 +3,8 @@
 // part of the product: librt_hw_amd.so has no CPU render path.
 #include <cstdint>
 #include <cstring>
-#include "../../raytracing-hw_amd/csrc/rt_path.h"
+#include <vector>
+#include "../../raytracing-hw_amd/csrc/rt_wave.h"
 #include "../../include/rt_hw.h"
 
 static rtd::DevScene make(const rt_scene_view *v) {
@@ -30,17 +31,99 @@ static rtd::DevScene make(const rt_scene_view *v) {
     return s;
 }
 
-extern "C" void kh_render(const rt_scene_view *v, int spp, int64_t p0, int64_t p1, float *out, uint64_t *cnt) {
+// render_pixel with the stepped traversal of the wave kernel (rt_wave.h)
+template <bool COUNT>
+static rtv::V3 render_pixel_stepped(const rtd::DevScene &sc, int i, int j, int spp, rtd::Counters &cnt) {
+    rtd::Rng rng;
+    uint32_t seed = (uint32_t)(j * sc.width + i) % 2147483647u;
+    rng.x = seed == 0 ? 1u : seed;
+    rng.saved_avail = 0;
+    rng.saved = 0.f;
+    rtv::V3 sum{0.f, 0.f, 0.f};
+    for (int s = 0; s < spp; ++s) {
+        float ox = rtd::rng_offset(rng);
+        float oy = rtd::rng_offset(rng);
+        rtd::Ray r = rtd::camera_ray(sc, i, j, ox, oy);
+        sum = rtv::add(sum, rtd::trace_sample_stepped<COUNT>(sc, r, rng, cnt));
+    }
+    return sum;
+}
+
+extern "C" void kh_render(const rt_scene_view *v, int spp, int64_t p0, int64_t p1, float *out, uint64_t *cnt, int stepped) {
     rtd::DevScene s = make(v);
     uint64_t c[6] = {0, 0, 0, 0, 0, 0};
 #pragma omp parallel for schedule(dynamic, 16) reduction(+ : c[:6])
     for (int64_t p = p0; p < p1; ++p) {
         rtd::Counters k{0, 0, 0, 0, 0, 0, 0};
-        rtv::V3 r = rtd::render_pixel<true>(s, (int)(p % v->width), (int)(p / v->width), spp, k);
+        rtv::V3 r = stepped ? render_pixel_stepped<true>(s, (int)(p % v->width), (int)(p / v->width), spp, k)
+                            : rtd::render_pixel<true>(s, (int)(p % v->width), (int)(p / v->width), spp, k);
         out[3 * (p - p0)] = r.x;
         out[3 * (p - p0) + 1] = r.y;
         out[3 * (p - p0) + 2] = r.z;
         c[0] += k.rays; c[1] += k.aabb; c[2] += k.tri; c[3] += k.lq; c[4] += k.laabb; c[5] += k.ltri;
     }
     std::memcpy(cnt, c, sizeof c);
+}
+
+// Emulates rt_wave_kernel (raytracing-hw_amd/csrc/rt_device.hip) on the host: `waves`
+// waves of 64 lanes run round-robin one main-loop iteration at a time, sharing the pixel
+// queue; every phase uses the same rt_wave.h lane functions as the device kernel.
+extern "C" int kh_render_wave(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
+                              float *out, uint64_t *cnt_out) {
+    rtd::DevScene sc = make(v);
+    int64_t rows = 0;
+    for (int r = 0; r < v->height; ++r)
+        if ((r / row_block) % world == rank) ++rows;
+    rtd::ShardGeom g{v->width, rank, world, row_block, (long long)rows * v->width};
+    std::vector<rtd::Lane> lanes((size_t)waves * 64);
+    std::vector<char> exhausted(waves, 0), done(waves, 0);
+    for (auto &L : lanes) rtd::lane_init(L);
+    rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    unsigned queue = 0;
+    int live = waves;
+    while (live > 0) {
+        for (int w = 0; w < waves; ++w) {
+            if (done[w]) continue;
+            rtd::Lane *W = &lanes[(size_t)w * 64];
+            if (!exhausted[w]) {
+                uint64_t m = 0;
+                for (int l = 0; l < 64; ++l) if (W[l].pix < 0) m |= 1ull << l;
+                if (m) {
+                    unsigned base = queue;
+                    unsigned cm = (unsigned)__builtin_popcountll(m);
+                    queue += cm;
+                    for (int l = 0; l < 64; ++l) {
+                        if (!(m >> l & 1)) continue;
+                        long long p = (long long)base + __builtin_popcountll(m & ((1ull << l) - 1ull));
+                        if (p < g.n_pixels) rtd::lane_assign(W[l], sc, g, p);
+                    }
+                    if ((long long)base + cm >= g.n_pixels) exhausted[w] = 1;
+                }
+            }
+            bool any = false;
+            for (int l = 0; l < 64; ++l) any |= W[l].pix >= 0;
+            if (!any) { done[w] = 1; --live; continue; }
+            for (int l = 0; l < 64; ++l)
+                if (W[l].pix >= 0 && W[l].state == rtd::L_IDLE) rtd::lane_start_sample<true>(W[l], sc, g, cnt);
+            bool trav[64];
+            for (int l = 0; l < 64; ++l) trav[l] = W[l].state == rtd::L_TRAV;
+            for (;;) {
+                bool a = false;
+                for (int l = 0; l < 64; ++l) a |= trav[l];
+                if (!a) break;
+                for (int l = 0; l < 64; ++l)
+                    if (trav[l]) {
+                        if (W[l].t.sp < 0 || W[l].t.sp >= rtd::kStack) return -1;
+                        trav[l] = rtd::trav_step<true>(sc, W[l].r, W[l].t, W[l].stk, cnt);
+                    }
+            }
+            for (int l = 0; l < 64; ++l) {
+                if (W[l].state == rtd::L_TRAV) W[l].state = rtd::L_SHADE;
+                if (W[l].state == rtd::L_SHADE) rtd::lane_shade<true>(W[l], sc, spp, out, cnt);
+            }
+        }
+    }
+    uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
+    std::memcpy(cnt_out, c, sizeof c);
+    return 0;
 }
