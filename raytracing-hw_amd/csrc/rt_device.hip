@@ -156,18 +156,7 @@ __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, 
     for (long long base = (long long)blockIdx.x * blockDim.x; base < st.n; base += (long long)gridDim.x * blockDim.x) {
         const long long i = base + threadIdx.x;
         const bool valid = i < st.n;
-        if (valid) {
-            const int k = (int)(i / g.width), px = (int)(i % g.width), py = shard_row(g, k);
-            const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;  // scene.cpp:34
-            rtd::Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
-            int power = 0;
-            const rtd::Ray r = rtd::start_sample(sc, g, i, rng, power);
-            rtd::store_ray(st, i, r);
-            st.sx[i] = st.sy[i] = st.sz[i] = 0.f;
-            st.rng_x[i] = rng.x;
-            st.rng_saved[i] = rng.saved;
-            st.meta[i] = rtd::meta_pack(0, power, 0, rng.saved_avail);
-        }
+        if (valid) rtd::wf_init_slot(sc, g, st, i);
         rtd::queue_push(valid, (int)i, queue, count);
     }
 }
@@ -178,18 +167,8 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfStat
     const unsigned n = *count;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 stk[rtd::kStack];
-    for (unsigned q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
-        const int i = queue[q];
-        const rtd::Ray r = rtd::load_ray(st, i);
-        rtd::Trav t;
-        if (rtd::trav_begin<COUNT>(sc, r, t, cnt))
-            while (rtd::trav_step<COUNT>(sc, r, t, stk, cnt)) {
-            }
-        st.hprim[i] = t.best.prim;
-        st.ht[i] = t.best.t;
-        st.hu[i] = t.best.u;
-        st.hv[i] = t.best.v;
-    }
+    for (unsigned q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x)
+        rtd::wf_extend_slot<COUNT>(sc, st, queue[q], stk, cnt);
     rtd::counters_flush<COUNT>(cnt, counters);
 }
 
@@ -203,43 +182,7 @@ __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc, ShardGeom g,
         const unsigned q = base + threadIdx.x;
         const bool valid = q < n;
         const int i = valid ? qin[q] : 0;
-        bool next = false;
-        if (valid) {
-            rtd::Ray r = rtd::load_ray(st, i);
-            const uint32_t meta = st.meta[i];
-            int s = (int)(meta & 0xfffffu), power = (int)((meta >> 20) & 15u), nv = (int)((meta >> 24) & 15u);
-            rtd::Rng rng{st.rng_x[i], (meta >> 28) & 1u, st.rng_saved[i]};
-            rtd::SoARec P{st.rec, st.n, (long long)i, st.D};
-            const rtd::Hit h{st.ht[i], st.hu[i], st.hv[i], st.hprim[i]};
-            // scene.cpp:85-154 for this vertex; the recursion goes on while calls remain
-            if (h.prim >= 0 && h.t < sc.max_distance && rtd::shade_hit<COUNT>(sc, r, h, rng, cnt, P, nv)) {
-                if (power > 0) {
-                    power -= 1;
-                    next = true;
-                }
-            }
-            if (!next) {
-                // path over: fold, accumulate (scene.cpp:41-42), next sample or pixel done
-                const rtv::V3 c = rtd::fold_path(P, nv);
-                const float ax = st.sx[i] + c.x, ay = st.sy[i] + c.y, az = st.sz[i] + c.z;
-                st.sx[i] = ax;
-                st.sy[i] = ay;
-                st.sz[i] = az;
-                if (++s == spp) {
-                    out[3 * (long long)i + 0] = ax;
-                    out[3 * (long long)i + 1] = ay;
-                    out[3 * (long long)i + 2] = az;
-                } else {
-                    r = rtd::start_sample(sc, g, i, rng, power);
-                    nv = 0;
-                    next = true;
-                }
-            }
-            if (next) rtd::store_ray(st, i, r);
-            st.meta[i] = rtd::meta_pack(s, power, nv, rng.saved_avail);
-            st.rng_x[i] = rng.x;
-            st.rng_saved[i] = rng.saved;
-        }
+        const bool next = valid && rtd::wf_shade_slot<COUNT>(sc, g, st, spp, i, out, cnt);
         rtd::queue_push(next, i, qout, cout);
     }
     rtd::counters_flush<COUNT>(cnt, counters);
@@ -272,8 +215,8 @@ __global__ void __launch_bounds__(256) rt_rays_kernel(DevScene sc, long long n, 
 namespace {
 
 template <class T>
-size_t append(std::vector<uint8_t> &blob, const std::vector<T> &v) {
-    size_t off = (blob.size() + 255) & ~size_t(255);
+size_t append(std::vector<uint8_t> &blob, const std::vector<T> &v, size_t pre = 0) {
+    size_t off = ((blob.size() + 255) & ~size_t(255)) + pre;
     blob.resize(off + v.size() * sizeof(T));
     if (!v.empty()) std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
     return off;
@@ -285,16 +228,24 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (s->bvh_depth + 2 >= (uint32_t)rtd::kStack || s->light_bvh_depth + 2 >= (uint32_t)rtd::kStack)
         return rt_fail(RT_ERR_LIMIT, "BVH deeper than the device traversal stack (" + std::to_string(rtd::kStack) + ")");
     if (s->ray_depth > rtd::kMaxDepth) return rt_fail(RT_ERR_LIMIT, "ray_depth exceeds device limit");
+    for (size_t k = 0; k < s->node.size() / 8; ++k) {  // wavefront traversal frame packing (rt_wavefront.h)
+        uint32_t a, b;
+        std::memcpy(&a, &s->node[8 * k + 6], 4);
+        std::memcpy(&b, &s->node[8 * k + 7], 4);
+        if (a >= rtd::kFrameMaxA || b >= 1024u)
+            return rt_fail(RT_ERR_LIMIT, "scene too large for the device BVH frame packing (2^22 nodes/triangles, 255 per leaf)");
+    }
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return rt_fail(RT_ERR_DEVICE, "no HIP device " + std::to_string(device));
     HIP_TRY(hipSetDevice(device));
     std::vector<uint8_t> blob;
     const size_t o_tri = append(blob, s->tri), o_attr = append(blob, s->tri_attr), o_tan = append(blob, s->tri_tan),
-                 o_node = append(blob, s->node), o_light = append(blob, s->light),
+                 o_node = append(blob, s->node, 32), o_light = append(blob, s->light),
                  o_lnode = append(blob, s->light_node), o_mf = append(blob, s->mesh_f),
                  o_mt = append(blob, s->mesh_tex), o_nt = append(blob, s->mesh_nt), o_ti = append(blob, s->tex_info),
                  o_tx = append(blob, s->texels);
+    // node array at +32 B: sibling pairs (left odd, left + 1) share one 64-B line
     blob.resize(((blob.size() + 255) & ~size_t(255)) + 256);
     rt_device_scene *d = new rt_device_scene();
     d->device = device;

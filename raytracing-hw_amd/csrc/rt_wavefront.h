@@ -35,6 +35,7 @@ __device__ __forceinline__ uint32_t meta_pack(int s, int power, int nv, uint32_t
     return (uint32_t)s | ((uint32_t)power << 20) | ((uint32_t)nv << 24) | (saved << 28);
 }
 
+#ifdef __HIPCC__
 // Appends `slot` to a queue when `want`: one atomic per wave, lanes keep their order.
 __device__ __forceinline__ void queue_push(bool want, int slot, int *queue, unsigned *count) {
     const unsigned long long m = __ballot(want);
@@ -58,6 +59,7 @@ __device__ __forceinline__ void counters_flush(const Counters &c, unsigned long 
         if ((threadIdx.x & 63) == 0 && x) atomicAdd(&out[k], x);
     }
 }
+#endif
 
 __device__ __forceinline__ void store_ray(const WfState &st, long long i, const Ray &r) {
     st.ox[i] = r.o.x; st.oy[i] = r.o.y; st.oz[i] = r.o.z;
@@ -72,6 +74,112 @@ __device__ __forceinline__ Ray load_ray(const WfState &st, long long i) {
     return r;
 }
 
+// ---------------------------------------------------------------- extend traversal
+// BVH::intersect (bvh.cpp:177-243) for the extend kernel.  Same visits, same counters and
+// same winner as closest_hit() in rt_path.h, with less memory traffic per internal node:
+//   * both children of a node are fetched together — they are siblings (left, left+1) and
+//     the device copy of the node array is offset so every sibling pair is one 64-B line;
+//   * both child boxes are tested on arrival.  The reference tests the far box only after
+//     the near subtree returns, but the test is a pure function of (ray, box) and is always
+//     executed, so computing it early changes nothing; only the cull `dist > near best`
+//     has to wait for the near subtree;
+//   * frames are 8 bytes and carry the far child itself (its a/b fields and entry distance),
+//     so resuming a node never re-reads it:
+//       far frame  (a << 10 | b, entry distance)  pushed when both children are hit;
+//       best frame (kFrameAcc,  node's near best)  pushed when the far child is entered
+//                                                  after a near subtree.
+//     No frame is needed when a node has only one child to visit: its local best starts at
+//     1e9, so merging it is the identity.
+constexpr uint32_t kFrameMaxA = (1u << 22) - 1;
+constexpr uint32_t kFrameAcc = 0xffffffffu;
+
+__device__ __forceinline__ void load_pair(const float4 *nodes, uint32_t left, NodeRec &L, NodeRec &R) {
+    const float4 p0 = nodes[2 * left], q0 = nodes[2 * left + 1], p1 = nodes[2 * left + 2], q1 = nodes[2 * left + 3];
+    L.mn[0] = p0.x; L.mn[1] = p0.y; L.mn[2] = p0.z; L.mx[0] = p0.w; L.mx[1] = q0.x; L.mx[2] = q0.y;
+    L.a = __float_as_uint(q0.z); L.b = __float_as_uint(q0.w);
+    R.mn[0] = p1.x; R.mn[1] = p1.y; R.mn[2] = p1.z; R.mx[0] = p1.w; R.mx[1] = q1.x; R.mx[2] = q1.y;
+    R.a = __float_as_uint(q1.z); R.b = __float_as_uint(q1.w);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const Ray &r, Hit &best, uint2 *stk, Counters &cnt) {
+    if (COUNT) { cnt.rays++; cnt.aabb++; }
+    best.t = 1e9f;
+    best.prim = -1;
+    best.u = best.v = 0.f;
+    const NodeRec root = load_node(sc.node, 0);
+    float e;
+    if (!aabb_hit(root.mn, root.mx, r, e)) return;
+    uint32_t a = root.a, b = root.b;
+    float acc = 1e9f;   // best t inside the subtree being traversed (the reference's local best)
+    int sp = 0;
+    for (;;) {
+        bool leaf = true;
+        while (b < 3u) {   // internal node: split axis in b, left child in a
+            RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, a = 0);
+            NodeRec L, R;
+            load_pair(sc.node, a, L, R);
+            if (COUNT) cnt.aabb += 2;
+            const float ds = b == 0 ? r.d.x : (b == 1 ? r.d.y : r.d.z);
+            const bool lf = ds > 0;
+            NodeRec N, F;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                N.mn[k] = lf ? L.mn[k] : R.mn[k]; N.mx[k] = lf ? L.mx[k] : R.mx[k];
+                F.mn[k] = lf ? R.mn[k] : L.mn[k]; F.mx[k] = lf ? R.mx[k] : L.mx[k];
+            }
+            N.a = lf ? L.a : R.a; N.b = lf ? L.b : R.b;
+            F.a = lf ? R.a : L.a; F.b = lf ? R.b : L.b;
+            float en, ef;
+            const bool hn = aabb_hit(N.mn, N.mx, r, en);
+            const bool hf = aabb_hit(F.mn, F.mx, r, ef);
+            if (hn) {
+                if (hf) {
+                    RT_CHECK(sp < kStack, 11, sp, sp = 0);
+                    stk[sp++] = make_uint2((F.a << 10) | F.b, __float_as_uint(ef));
+                }
+                a = N.a; b = N.b;
+            } else if (hf && !(ef > 1e9f)) {
+                a = F.a; b = F.b;
+            } else {
+                leaf = false;
+                break;
+            }
+        }
+        if (leaf) {
+            const uint32_t kend = a + (b >> 2);
+            RT_CHECK(kend <= (uint32_t)sc.n_tris, 12, kend, a = kend);
+            for (uint32_t k = a; k < kend; ++k) {
+                V3 v0, U, V;
+                load_tri(sc.tri, (int)k, v0, U, V);
+                TriHit h;
+                if (COUNT) cnt.tri++;
+                if (tri_hit(v0, U, V, r, h)) {
+                    if (h.t < acc) acc = h.t;
+                    if (h.t < best.t) { best.t = h.t; best.u = h.u; best.v = h.v; best.prim = (int)k; }
+                }
+            }
+        }
+        // return: merge subtree bests upwards until a far child is to be visited
+        for (;;) {
+            if (sp == 0) return;
+            const uint2 f = stk[--sp];
+            if (f.x == kFrameAcc) {
+                const float p = __uint_as_float(f.y);
+                acc = acc < p ? acc : p;
+                continue;
+            }
+            if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
+                stk[sp++] = make_uint2(kFrameAcc, __float_as_uint(acc));
+                a = f.x >> 10;
+                b = f.x & 1023u;
+                acc = 1e9f;
+                break;
+            }
+        }
+    }
+}
+
 // Start sample s of slot i: jittered camera ray (scene.cpp:36-39); the first traversal
 // consumes one call of the depth budget (scene.cpp:72-75).
 __device__ __forceinline__ Ray start_sample(const DevScene &sc, const ShardGeom &g, long long i, Rng &rng, int &power) {
@@ -80,6 +188,79 @@ __device__ __forceinline__ Ray start_sample(const DevScene &sc, const ShardGeom 
     const float oy = rng_offset(rng);
     power = sc.ray_depth - 1;
     return camera_ray(sc, px, py, ox, oy);
+}
+
+// ---------------------------------------------------------------- per-slot bodies
+// The three kernels in rt_device.hip are these functions plus queue compaction; the host
+// test harness (tests/native/kernel_host.cpp) runs the same functions with a host queue.
+
+// wf_init: seed slot i's RNG from its pixel (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1)
+// and start its first sample.
+__device__ __forceinline__ void wf_init_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, long long i) {
+    const int k = (int)(i / g.width), px = (int)(i % g.width), py = shard_row(g, k);
+    const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
+    Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
+    int power = 0;
+    const Ray r = start_sample(sc, g, i, rng, power);
+    store_ray(st, i, r);
+    st.sx[i] = st.sy[i] = st.sz[i] = 0.f;
+    st.rng_x[i] = rng.x;
+    st.rng_saved[i] = rng.saved;
+    st.meta[i] = meta_pack(0, power, 0, rng.saved_avail);
+}
+
+// wf_extend: closest hit of slot i's current ray.
+template <bool COUNT>
+__device__ __forceinline__ void wf_extend_slot(const DevScene &sc, const WfState &st, long long i, uint2 *stk,
+                                               Counters &cnt) {
+    const Ray r = load_ray(st, i);
+    Hit h;
+    closest_hit_wf<COUNT>(sc, r, h, stk, cnt);
+    st.hprim[i] = h.prim;
+    st.ht[i] = h.t;
+    st.hu[i] = h.u;
+    st.hv[i] = h.v;
+}
+
+// wf_shade: one vertex of scene.cpp:85-154 for slot i, then bounce (true: the slot has a
+// new ray to extend) or end the path: fold it, add it to the pixel sum (scene.cpp:41-42)
+// and start the next sample, or write the pixel after the last one (false).
+template <bool COUNT>
+__device__ __forceinline__ bool wf_shade_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, int spp,
+                                              long long i, float *out, Counters &cnt) {
+    Ray r = load_ray(st, i);
+    const uint32_t meta = st.meta[i];
+    int s = (int)(meta & 0xfffffu), power = (int)((meta >> 20) & 15u), nv = (int)((meta >> 24) & 15u);
+    Rng rng{st.rng_x[i], (meta >> 28) & 1u, st.rng_saved[i]};
+    SoARec P{st.rec, st.n, i, st.D};
+    const Hit h{st.ht[i], st.hu[i], st.hv[i], st.hprim[i]};
+    bool next = false;
+    // the recursion continues with the bounce ray while calls remain (scene.cpp:72-75)
+    if (h.prim >= 0 && h.t < sc.max_distance && shade_hit<COUNT>(sc, r, h, rng, cnt, P, nv) && power > 0) {
+        power -= 1;
+        next = true;
+    }
+    if (!next) {
+        const V3 c = fold_path(P, nv);
+        const float ax = st.sx[i] + c.x, ay = st.sy[i] + c.y, az = st.sz[i] + c.z;
+        st.sx[i] = ax;
+        st.sy[i] = ay;
+        st.sz[i] = az;
+        if (++s == spp) {
+            out[3 * i + 0] = ax;
+            out[3 * i + 1] = ay;
+            out[3 * i + 2] = az;
+        } else {
+            r = start_sample(sc, g, i, rng, power);
+            nv = 0;
+            next = true;
+        }
+    }
+    if (next) store_ray(st, i, r);
+    st.meta[i] = meta_pack(s, power, nv, rng.saved_avail);
+    st.rng_x[i] = rng.x;
+    st.rng_saved[i] = rng.saved;
+    return next;
 }
 
 }  // namespace rtd

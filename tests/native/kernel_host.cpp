@@ -4,7 +4,7 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
-#include "../../raytracing-hw_amd/csrc/rt_wave.h"
+#include "../../raytracing-hw_amd/csrc/rt_wavefront.h"
 #include "../../include/rt_hw.h"
 
 static rtd::DevScene make(const rt_scene_view *v) {
@@ -125,5 +125,50 @@ extern "C" int kh_render_wave(const rt_scene_view *v, int spp, int rank, int wor
     }
     uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
     std::memcpy(cnt_out, c, sizeof c);
+    return 0;
+}
+
+// Emulates the wavefront path (wf_init / wf_extend / wf_shade in rt_device.hip) on the host:
+// the same rt_wavefront.h slot functions over SoA state, driven by a host queue.
+extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world, int row_block, float *out,
+                            uint64_t *cnt_out, int64_t *iterations) {
+    rtd::DevScene sc = make(v);
+    sc.n_tris = (int)v->n_tris;
+    sc.n_nodes = (int)v->n_nodes;
+    int64_t rows = 0;
+    for (int r = 0; r < v->height; ++r)
+        if ((r / row_block) % world == rank) ++rows;
+    const long long n = (long long)rows * v->width;
+    rtd::ShardGeom g{v->width, rank, world, row_block, n};
+    const int D = v->ray_depth;
+    std::vector<float> f((size_t)n * (13 + 9 * D));
+    std::vector<uint32_t> u((size_t)n * 3);
+    rtd::WfState st{};
+    st.n = n;
+    st.D = D;
+    float *fp = f.data();
+    float **planes[] = {&st.ox, &st.oy, &st.oz, &st.dx, &st.dy, &st.dz, &st.ht, &st.hu, &st.hv, &st.rng_saved,
+                        &st.sx, &st.sy, &st.sz};
+    for (float **pp : planes) { *pp = fp; fp += n; }
+    st.rec = fp;
+    st.hprim = (int *)u.data();
+    st.rng_x = u.data() + n;
+    st.meta = u.data() + 2 * n;
+    std::vector<int> q, q2;
+    for (long long i = 0; i < n; ++i) { rtd::wf_init_slot(sc, g, st, i); q.push_back((int)i); }
+    rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    uint2 stk[rtd::kStack];
+    int64_t it = 0;
+    while (!q.empty()) {
+        if (++it > (int64_t)spp * D + 16) return -1;
+        for (int i : q) rtd::wf_extend_slot<true>(sc, st, i, stk, cnt);
+        q2.clear();
+        for (int i : q)
+            if (rtd::wf_shade_slot<true>(sc, g, st, spp, i, out, cnt)) q2.push_back(i);
+        q.swap(q2);
+    }
+    uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
+    std::memcpy(cnt_out, c, sizeof c);
+    if (iterations) *iterations = it;
     return 0;
 }

@@ -1,0 +1,103 @@
+"""The GPU kernel source, compiled for the host (tests/native/kernel_host.cpp), against the
+reference's own per-pixel sums and counters (tests/golden, made by oracle/ref_harness).
+
+Three schedules of the same per-pixel arithmetic are checked bit-exactly:
+  * render_pixel      (rt_path.h, kernels 1 and 2: recursive-order closest_hit),
+  * stepped traversal (rt_wave.h, the wave megakernel's trav_step),
+  * wavefront         (rt_wavefront.h slot functions, the default render path:
+                       closest_hit_wf with both-children fetch and 8-byte frames),
+plus the wave-kernel emulation with several waves sharing the pixel queue.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import rtref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "native", "kernel_host.cpp")
+CASES = [("cornell", 33, 17, 3), ("cornell", 64, 64, 8), ("cornell_blob", 48, 48, 4),
+         ("practice6_1", 256, 256, 4), ("sponza_mini", 64, 36, 4)]
+FAST = [("cornell", 33, 17, 3), ("cornell_blob", 48, 48, 4), ("sponza_mini", 64, 36, 4)]
+
+
+@pytest.fixture(scope="module")
+def kh(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("kh") / "libkh.so")
+    subprocess.run(["g++", "-O2", "-fno-tree-vectorize", "-fno-tree-slp-vectorize", "-ffp-contract=off", "-fopenmp",
+                    "-std=c++17", "-shared", "-fPIC", SRC, "-o", out], check=True)
+    lib = ctypes.CDLL(out)
+    V, I, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    lib.kh_render.argtypes = [V, I, L, L, V, V, I]
+    lib.kh_render.restype = None
+    lib.kh_render_wave.argtypes = [V, I, I, I, I, I, V, V]
+    lib.kh_render_wave.restype = I
+    lib.kh_render_wf.argtypes = [V, I, I, I, I, V, V, V]
+    lib.kh_render_wf.restype = I
+    return lib
+
+
+def _golden(name, w, h, s):
+    g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
+    return g["sums"].reshape(h * w, 3), g["counters"]
+
+
+def _view(rt, name, w, h, s):
+    return rt.make_view(rtref.ref_arrays(rt, name, w, h, s))
+
+
+@pytest.mark.parametrize("name,w,h,s", CASES)
+@pytest.mark.parametrize("stepped", [0, 1])
+def test_pixel_schedules_match_reference(rt, kh, name, w, h, s, stepped):
+    if stepped and (name, w, h, s) not in FAST:
+        pytest.skip("stepped traversal covered on the fast cases")
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    out = np.zeros((h * w, 3), np.float32)
+    cnt = np.zeros(6, np.uint64)
+    kh.kh_render(ctypes.addressof(v), s, 0, w * h, out.ctypes.data, cnt.ctypes.data, stepped)
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert list(cnt) == list(cnt_want)
+
+
+@pytest.mark.parametrize("name,w,h,s", CASES)
+def test_wavefront_matches_reference(rt, kh, name, w, h, s):
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    out = np.zeros((h * w, 3), np.float32)
+    cnt = np.zeros(7, np.uint64)
+    it = np.zeros(1, np.int64)
+    assert kh.kh_render_wf(ctypes.addressof(v), s, 0, 1, 8, out.ctypes.data, cnt.ctypes.data, it.ctypes.data) == 0
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert list(cnt[:6]) == list(cnt_want)
+    assert it[0] <= s * int(v.ray_depth) + 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wavefront_shards_reassemble(rt, kh, world):
+    name, w, h, s = "cornell", 33, 17, 3
+    want, _ = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    frame = np.zeros((h, w, 3), np.float32)
+    for rank in range(world):
+        rows = [r for r in range(h) if (r // 4) % world == rank]
+        out = np.zeros((len(rows) * w, 3), np.float32)
+        cnt = np.zeros(7, np.uint64)
+        assert kh.kh_render_wf(ctypes.addressof(v), s, rank, world, 4, out.ctypes.data, cnt.ctypes.data, None) == 0
+        frame[rows] = out.reshape(len(rows), w, 3)
+    assert np.array_equal(rtref.bits(frame.reshape(-1, 3)), rtref.bits(want))
+
+
+@pytest.mark.parametrize("waves", [1, 3])
+def test_wave_kernel_emulation(rt, kh, waves):
+    name, w, h, s = "cornell_blob", 48, 48, 4
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    out = np.zeros((h * w, 3), np.float32)
+    cnt = np.zeros(7, np.uint64)
+    assert kh.kh_render_wave(ctypes.addressof(v), s, 0, 1, 8, waves, out.ctypes.data, cnt.ctypes.data) == 0
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert list(cnt[:6]) == list(cnt_want)
