@@ -9,9 +9,11 @@ followed by the RCCL all-gather of the float framebuffer.  Rank 0 prints one JSO
 
 value    = scene closest-hit queries (rays, counted in-kernel during warmup; the count is
            deterministic per frame) of all ranks x K / max-over-ranks wall time of the K steps
-roofline = algorithmic bytes of rank 0's render kernel (24 B per AABB test + 36 B per
-           triangle test, scene and light BVH, + 156 B per shaded hit) per
-           launch / its average HIP-event duration, against the 8 TB/s HBM3E peak.
+roofline = the dominant kernel of rank 0 (wf_extend, the BVH traversal): algorithmic bytes
+           per launch (24 B per AABB test + 36 B per triangle test + 44 B of ray/hit I/O per
+           ray) / its average launch duration (HIP events around every launch in
+           the timed steps), against the 8 TB/s HBM3E peak.  path_* = the whole-path model
+           of SURVEY.md §8d (scene + light BVH + 156 B per shaded hit) over the frame time.
 cpu_baseline: the reference itself (oracle/_ref/ref_harness, built from /root/reference's
            sources) timing Scene::render on the host cores over a bounded sample of the same
            frame; falls back to the build's CPU restatement (oracle/) when _ref is absent.
@@ -30,6 +32,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_AABB, B_TRI, B_SHADE = 24, 36, 156
+B_RAY_IO = 24 + 4 + 16     # wf_extend per ray: ray (6 floats) + queue slot in, hit (t, u, v, prim) out
 
 
 def import_pkg():
@@ -128,7 +131,7 @@ def main():
 
     def step(count=False):
         st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
-                                 count=count, kernel=args.kernel, stats=True)
+                                 count=count, kernel=args.kernel, stats=True, kernel_times=not count)
         rtdist.gather_frame(out, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
         return st
 
@@ -140,13 +143,16 @@ def main():
             counts = st
     torch.cuda.synchronize()
 
-    kernel_ms = []
+    kernel_ms, ext_ms, ext_n, ext_rays = [], [], [], []
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         kernel_ms.append(st["render_ms"])
+        ext_ms.append(st["extend_ms"])
+        ext_n.append(st["extend_launches"])
+        ext_rays.append(st["extend_rays"])
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -165,9 +171,19 @@ def main():
         value = rays_per_frame * args.steps / elapsed / 1e6
         # rank 0's own kernel: algorithmic bytes per launch / average launch time
         c0 = counts
-        bytes_launch = (B_AABB * (c0["aabb_tests"] + c0["light_aabb_tests"]) + B_TRI * (c0["tri_tests"] + c0["light_tri_tests"])
-                        + B_SHADE * c0["shading_hits"])
-        avg_s = float(np.mean(kernel_ms)) / 1e3
+        # whole path: every BVH node / triangle record + shading fetch per frame
+        bytes_frame = (B_AABB * (c0["aabb_tests"] + c0["light_aabb_tests"]) + B_TRI * (c0["tri_tests"] + c0["light_tri_tests"])
+                       + B_SHADE * c0["shading_hits"])
+        frame_s = float(np.mean(kernel_ms)) / 1e3
+        if args.kernel == 0 and sum(ext_n) > 0:
+            # dominant kernel = wf_extend: scene-BVH node pairs + triangles + per-ray SoA in/out
+            ext_bytes = B_AABB * c0["aabb_tests"] + B_TRI * c0["tri_tests"] + B_RAY_IO * ext_rays[0]
+            launches = float(np.mean(ext_n))
+            bytes_launch = ext_bytes / launches
+            avg_s = float(np.sum(ext_ms)) / float(np.sum(ext_n)) / 1e3
+            kname = "wf_extend_kernel"
+        else:
+            bytes_launch, avg_s, launches, kname = bytes_frame, frame_s, 1.0, "render kernel"
         achieved = bytes_launch / avg_s / 1e9
         line = {
             "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",
@@ -191,7 +207,10 @@ def main():
                        "scene_load_s": round(load_s, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_launch": int(bytes_launch), "kernel_ms": round(avg_s * 1e3, 3)},
+                         "kernel": kname, "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
+                         "launches_per_frame": launches,
+                         "path_frame_bytes": int(bytes_frame), "path_frame_ms": round(frame_s * 1e3, 3),
+                         "path_achieved": round(bytes_frame / frame_s / 1e9, 1)},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum rt_status {
     RT_OK = 0,
@@ -86,8 +86,12 @@ typedef struct {
     int32_t row_block;    /* rows per interleave block (default 8)                       */
     int32_t count;        /* 1 = accumulate ray / AABB / triangle test counters          */
     int32_t kernel;       /* 0 = wavefront (default), 1 = one lane per pixel, 2 = persistent per-pixel, 3 = wave megakernel */
-    int32_t reserved[2];
+    int32_t flags;        /* RT_FLAG_* */
+    int32_t reserved;
 } rt_params;
+
+/* rt_params.flags */
+#define RT_FLAG_KERNEL_TIMES 1  /* wavefront path: time every extend / shade launch (HIP events) */
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */
@@ -100,6 +104,10 @@ typedef struct {
     uint64_t light_tri_tests;
     uint64_t shading_hits;  /* scene hits that were shaded (texture / attribute fetches)  */
     double render_ms;       /* device time of the render kernel(s), HIP events            */
+    /* RT_FLAG_KERNEL_TIMES (wavefront path): summed launch durations and launch counts   */
+    double extend_ms, shade_ms;
+    uint64_t extend_launches, shade_launches;
+    uint64_t extend_rays;   /* rays traced by the extend launches (always filled)          */
 } rt_stats;
 
 /* --- scene ------------------------------------------------------------------------ */

@@ -44,17 +44,22 @@ class RtSceneView(ctypes.Structure):
     ]
 
 
+ABI_VERSION = 2          # include/rt_hw.h RT_ABI_VERSION
+FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES
+
+
 class RtParams(ctypes.Structure):
     _fields_ = [("spp", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("row_block", ctypes.c_int32), ("count", ctypes.c_int32), ("kernel", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class RtStats(ctypes.Structure):
     _fields_ = [("pixels", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("rays", ctypes.c_uint64),
                 ("aabb_tests", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("light_queries", ctypes.c_uint64),
                 ("light_aabb_tests", ctypes.c_uint64), ("light_tri_tests", ctypes.c_uint64), ("shading_hits", ctypes.c_uint64),
-                ("render_ms", ctypes.c_double)]
+                ("render_ms", ctypes.c_double), ("extend_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
+                ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64), ("extend_rays", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -195,8 +200,8 @@ class Scene:
     def upload(self, device=0):
         _check(lib().rt_scene_upload(self._h, device))
 
-    def _params(self, spp, rank, world, row_block, count, kernel):
-        return RtParams(spp or 0, rank, world, row_block, int(count), kernel)
+    def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False):
+        return RtParams(spp or 0, rank, world, row_block, int(count), kernel, FLAG_KERNEL_TIMES if kernel_times else 0)
 
     def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0):
         """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42)."""
@@ -209,9 +214,10 @@ class Scene:
         return out, st.as_dict()
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
-                      kernel=0, stats=False):
-        """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream."""
-        p = self._params(spp, rank, world, row_block, count, kernel)
+                      kernel=0, stats=False, kernel_times=False):
+        """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream.
+        kernel_times: per-launch HIP-event timing of the wavefront kernels (needs stats)."""
+        p = self._params(spp, rank, world, row_block, count, kernel, kernel_times)
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))

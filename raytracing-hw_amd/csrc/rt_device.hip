@@ -165,6 +165,7 @@ template <bool COUNT>
 __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfState st, const int *queue,
                                                          const unsigned *count, unsigned long long *counters) {
     const unsigned n = *count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 stk[rtd::kStack];
     for (unsigned q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x)
@@ -337,8 +338,42 @@ unsigned persistent_blocks(rt_device_scene *d, K kernel, long long work) {
     return (unsigned)std::max<long long>(b, 1);
 }
 
+// Per-launch HIP events for RT_FLAG_KERNEL_TIMES.
+struct LaunchTimer {
+    bool on = false;
+    std::vector<hipEvent_t> ev[2];   // [kernel]: start, end, start, end, ...
+    hipError_t mark(int k, hipStream_t s) {
+        if (!on) return hipSuccess;
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        ev[k].push_back(e);
+        return hipEventRecord(e, s);
+    }
+    // sums the durations (after the stream has drained) and releases the events
+    hipError_t collect(double ms[2], uint64_t n[2]) {
+        hipError_t r = hipSuccess;
+        for (int k = 0; k < 2; ++k) {
+            ms[k] = 0.0;
+            n[k] = ev[k].size() / 2;
+            for (size_t j = 0; j + 1 < ev[k].size(); j += 2) {
+                float t = 0.f;
+                if (r == hipSuccess) r = hipEventElapsedTime(&t, ev[k][j], ev[k][j + 1]);
+                ms[k] += t;
+            }
+            for (hipEvent_t e : ev[k]) (void)hipEventDestroy(e);
+            ev[k].clear();
+        }
+        return r;
+    }
+    ~LaunchTimer() {
+        for (auto &v : ev)
+            for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    }
+};
+
 int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth, float *d_out, hipStream_t stream,
-                     bool count) {
+                     bool count, LaunchTimer &timer) {
     if (depth < 1 || depth > 15) return rt_fail(RT_ERR_LIMIT, "wavefront path: ray_depth must be in [1, 15]");
     if (spp >= (1 << 20)) return rt_fail(RT_ERR_LIMIT, "wavefront path: spp must be < 2^20");
     int rc = ensure_wf(d, g.n_pixels, depth);
@@ -358,13 +393,14 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     for (long long it = 0;; ++it) {
         if (it > max_iter) return rt_fail(RT_ERR_DEVICE, "wavefront path did not drain (internal error)");
         HIP_TRY(hipMemsetAsync(&d->wf_count[1 - cur], 0, 4, stream));
-        if (count) {
-            hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
-            hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
-        } else {
-            hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
-            hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
-        }
+        HIP_TRY(timer.mark(0, stream));
+        if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
+        else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
+        HIP_TRY(timer.mark(0, stream));
+        HIP_TRY(timer.mark(1, stream));
+        if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
+        else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
+        HIP_TRY(timer.mark(1, stream));
         HIP_TRY(hipGetLastError());
         cur = 1 - cur;
         if ((it & 7) == 7) {
@@ -388,7 +424,9 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
     rt_device_scene *d = s->dev;
     HIP_TRY(hipSetDevice(d->device));
     const bool count = p->count != 0;
-    if (count) HIP_TRY(hipMemsetAsync(d->counters, 0, 8 * sizeof(unsigned long long), stream));
+    if (count || st) HIP_TRY(hipMemsetAsync(d->counters, 0, 8 * sizeof(unsigned long long), stream));
+    LaunchTimer timer;
+    timer.on = st != nullptr && (p->flags & RT_FLAG_KERNEL_TIMES) != 0;
     HIP_TRY(hipMemsetAsync(d->queue, 0, 4, stream));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (st) {
@@ -409,7 +447,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (count) hipLaunchKernelGGL(rt_persistent_kernel<true>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
             else hipLaunchKernelGGL(rt_persistent_kernel<false>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
         } else if (p->kernel == 0) {
-            int rc = launch_wavefront(d, g, spp, s->ray_depth, d_out, stream, count);
+            int rc = launch_wavefront(d, g, spp, s->ray_depth, d_out, stream, count, timer);
             if (rc) return rc;
         } else {
             // persistent wave kernel: exactly the resident blocks (occupancy query), capped by the work
@@ -436,9 +474,17 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
         st->pixels = (uint64_t)g.n_pixels;
         st->samples = (uint64_t)g.n_pixels * (uint64_t)spp;
         st->render_ms = ms;
+        double kms[2];
+        uint64_t kn[2];
+        HIP_TRY(timer.collect(kms, kn));
+        st->extend_ms = kms[0];
+        st->shade_ms = kms[1];
+        st->extend_launches = kn[0];
+        st->shade_launches = kn[1];
+        unsigned long long c[8];
+        HIP_TRY(hipMemcpy(c, d->counters, sizeof c, hipMemcpyDeviceToHost));
+        st->extend_rays = c[7];
         if (count) {
-            unsigned long long c[8];
-            HIP_TRY(hipMemcpy(c, d->counters, sizeof c, hipMemcpyDeviceToHost));
             st->rays = c[0]; st->aabb_tests = c[1]; st->tri_tests = c[2];
             st->light_queries = c[3]; st->light_aabb_tests = c[4]; st->light_tri_tests = c[5];
             st->shading_hits = c[6];
