@@ -161,23 +161,68 @@ __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, 
     }
 }
 
+// Persistent traversal over the queue: every lane runs rounds of its own ray (rt_wavefront.h
+// trav_round); lanes whose ray finished take the next queued ray between rounds (one atomic
+// per wave), so a wave is never held by its slowest ray.
+constexpr int kLdsStack = 8;
 template <bool COUNT>
 __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfState st, const int *queue,
-                                                         const unsigned *count, unsigned long long *counters) {
+                                                         const unsigned *count, unsigned *fetch, unsigned *next_count,
+                                                         unsigned long long *counters) {
+    __shared__ uint2 lds_stack[kLdsStack * 256];
     const unsigned n = *count;
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
+        *next_count = 0;                                 // the shade kernel's output queue
+    }
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    uint2 stk[rtd::kStack];
-    for (unsigned q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x)
-        rtd::wf_extend_slot<COUNT>(sc, st, queue[q], stk, cnt);
+    rtd::LdsStack<kLdsStack> S{&lds_stack[threadIdx.x], {}};
+    const int lane = threadIdx.x & 63;
+    int slot = -1;
+    bool exhausted = false;
+    rtd::Ray r;
+    rtd::TravState T;
+    for (;;) {
+        const unsigned long long m = __ballot(slot < 0);
+        if (m && !exhausted) {
+            const int leader = __ffsll(m) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(fetch, (unsigned)__popcll(m));
+            base = __shfl(base, leader, 64);
+            exhausted = base + (unsigned)__popcll(m) >= n;
+            if (slot < 0) {
+                const unsigned q = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                if (q < n) {
+                    slot = queue[q];
+                    r = rtd::load_ray(st, slot);
+                    if (!rtd::trav_start<COUNT>(sc, r, T, cnt)) {
+                        st.hprim[slot] = -1;   // misses the scene box
+                        st.ht[slot] = T.best.t;
+                        st.hu[slot] = 0.f;
+                        st.hv[slot] = 0.f;
+                        slot = -1;
+                    }
+                }
+            }
+        }
+        if (slot >= 0 && rtd::trav_round<COUNT>(sc, r, T, S, cnt)) {
+            st.hprim[slot] = T.best.prim;
+            st.ht[slot] = T.best.t;
+            st.hu[slot] = T.best.u;
+            st.hv[slot] = T.best.v;
+            slot = -1;
+        }
+        if (exhausted && !__any(slot >= 0)) break;
+    }
     rtd::counters_flush<COUNT>(cnt, counters);
 }
 
 template <bool COUNT>
 __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp,
                                                         const int *qin, const unsigned *cin, int *qout, unsigned *cout,
-                                                        float *out, unsigned long long *counters) {
+                                                        unsigned *fetch, float *out, unsigned long long *counters) {
     const unsigned n = *cin;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fetch = 0;   // the next extend launch's ray counter
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     for (unsigned base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const unsigned q = base + threadIdx.x;
@@ -380,7 +425,7 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     if (rc) return rc;
     rtd::WfState w = d->wf;
     w.n = g.n_pixels;
-    HIP_TRY(hipMemsetAsync(d->wf_count, 0, 8, stream));
+    HIP_TRY(hipMemsetAsync(d->wf_count, 0, 16, stream));   // counts [0], [1]; extend ray counter [2]
     const unsigned init_blocks = (unsigned)std::min<long long>((g.n_pixels + 255) / 256, (long long)d->cu_count * 8);
     hipLaunchKernelGGL(wf_init_kernel, dim3(init_blocks), dim3(256), 0, stream, d->ds, g, w, d->wf_queue[0], &d->wf_count[0]);
     HIP_TRY(hipGetLastError());
@@ -392,14 +437,13 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     int cur = 0;
     for (long long it = 0;; ++it) {
         if (it > max_iter) return rt_fail(RT_ERR_DEVICE, "wavefront path did not drain (internal error)");
-        HIP_TRY(hipMemsetAsync(&d->wf_count[1 - cur], 0, 4, stream));
         HIP_TRY(timer.mark(0, stream));
-        if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
-        else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], d->counters);
+        if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], &d->wf_count[2], &d->wf_count[1 - cur], d->counters);
+        else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], &d->wf_count[2], &d->wf_count[1 - cur], d->counters);
         HIP_TRY(timer.mark(0, stream));
         HIP_TRY(timer.mark(1, stream));
-        if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
-        else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], d_out, d->counters);
+        if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
+        else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
         HIP_TRY(timer.mark(1, stream));
         HIP_TRY(hipGetLastError());
         cur = 1 - cur;

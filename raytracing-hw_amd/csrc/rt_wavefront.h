@@ -101,83 +101,204 @@ __device__ __forceinline__ void load_pair(const float4 *nodes, uint32_t left, No
     R.a = __float_as_uint(q1.z); R.b = __float_as_uint(q1.w);
 }
 
-template <bool COUNT>
-__device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const Ray &r, Hit &best, uint2 *stk, Counters &cnt) {
-    if (COUNT) { cnt.rays++; cnt.aabb++; }
-    best.t = 1e9f;
-    best.prim = -1;
-    best.u = best.v = 0.f;
-    const NodeRec root = load_node(sc.node, 0);
-    float e;
-    if (!aabb_hit(root.mn, root.mx, r, e)) return;
-    uint32_t a = root.a, b = root.b;
-    float acc = 1e9f;   // best t inside the subtree being traversed (the reference's local best)
-    int sp = 0;
-    for (;;) {
-        bool leaf = true;
-        while (b < 3u) {   // internal node: split axis in b, left child in a
-            RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, a = 0);
-            NodeRec L, R;
-            load_pair(sc.node, a, L, R);
-            if (COUNT) cnt.aabb += 2;
-            const float ds = b == 0 ? r.d.x : (b == 1 ? r.d.y : r.d.z);
-            const bool lf = ds > 0;
-            NodeRec N, F;
+// aabb_hit() (rt_path.h; AABB::intersect, primitive.cpp:146-208) without branches: every
+// lane evaluates the same operations and the early returns become selects, so a wave does
+// not serialise on the inside / behind / outside cases.  Identical results; the entry
+// distance (a sqrt) only when DIST.
+template <bool DIST>
+__device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], const Ray &r, float &dist) {
+    const float o[3] = {r.o.x, r.o.y, r.o.z};
+    const float d[3] = {r.d.x, r.d.y, r.d.z};
+    const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+    bool inside = true;
+    bool mid[3];
+    float cand[3], maxT[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                N.mn[k] = lf ? L.mn[k] : R.mn[k]; N.mx[k] = lf ? L.mx[k] : R.mx[k];
-                F.mn[k] = lf ? R.mn[k] : L.mn[k]; F.mx[k] = lf ? R.mx[k] : L.mx[k];
-            }
-            N.a = lf ? L.a : R.a; N.b = lf ? L.b : R.b;
-            F.a = lf ? R.a : L.a; F.b = lf ? R.b : L.b;
-            float en, ef;
-            const bool hn = aabb_hit(N.mn, N.mx, r, en);
-            const bool hf = aabb_hit(F.mn, F.mx, r, ef);
-            if (hn) {
-                if (hf) {
-                    RT_CHECK(sp < kStack, 11, sp, sp = 0);
-                    stk[sp++] = make_uint2((F.a << 10) | F.b, __float_as_uint(ef));
-                }
-                a = N.a; b = N.b;
-            } else if (hf && !(ef > 1e9f)) {
-                a = F.a; b = F.b;
-            } else {
-                leaf = false;
-                break;
-            }
+    for (int i = 0; i < 3; ++i) {
+        const bool lo = o[i] < mn[i];
+        const bool hi = !lo && o[i] > mx[i];
+        mid[i] = !lo && !hi;
+        cand[i] = lo ? mn[i] : (hi ? mx[i] : 0.f);
+        inside = inside && mid[i];
+        maxT[i] = (!mid[i] && d[i] != 0.f) ? (cand[i] - o[i]) * inv[i] : -1.f;
+    }
+    int wp = maxT[0] < maxT[1] ? 1 : 0;
+    const float t01 = wp ? maxT[1] : maxT[0];
+    wp = t01 < maxT[2] ? 2 : wp;
+    const float tw = wp == 2 ? maxT[2] : t01;
+    bool out = tw < 0.f;
+    float coord[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float c = o[i] + tw * d[i];
+        const bool on = wp == i;
+        coord[i] = on ? cand[i] : c;
+        out = out || (!on && (c < mn[i] || c > mx[i]));
+    }
+    if (DIST) {
+        const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
+        dist = inside ? 0.f : l;
+    }
+    return inside || !out;
+}
+
+// tri_hit() (rt_path.h; Primitive::intersect, primitive.cpp:17-57) as selects.
+__device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriHit &h) {
+    const V3 p = rtv::cross(r.d, V);
+    const float det = rtv::dot(U, p);
+    const bool ok_det = !(-1e-6 < (double)det && (double)det < 1e-6);
+    const float inv_det = 1.f / det;
+    const V3 s = rtv::sub(r.o, v0);
+    const float u = inv_det * rtv::dot(s, p);
+    const V3 q = rtv::cross(s, U);
+    const float v = inv_det * rtv::dot(r.d, q);
+    const float t = inv_det * rtv::dot(V, q);
+    h.t = t;
+    h.u = u;
+    h.v = v;
+    return ok_det && !(u < 0 || u > 1) && !(v < 0 || u + v > 1) && !(t < 0.f);
+}
+
+// Resumable traversal state of one ray.
+struct TravState {
+    uint32_t a, b;   // node being entered: internal (b = split axis, a = left child) or leaf (b = 3 | n << 2, a = first)
+    float acc;       // best t inside the subtree being traversed (the reference's local best)
+    int sp;
+    Hit best;        // global winner so far (strict <, first of equal t wins)
+};
+
+// Host / test stack: a plain array.
+struct ArrayStack {
+    uint2 *p;
+    __device__ __forceinline__ void put(int i, uint2 v) { p[i] = v; }
+    __device__ __forceinline__ uint2 get(int i) const { return p[i]; }
+};
+
+// BVH::intersect entry (bvh.cpp:239-243): counters, root box.  False = the ray misses the
+// scene (T.best says so).
+template <bool COUNT>
+__device__ __forceinline__ bool trav_start(const DevScene &sc, const Ray &r, TravState &T, Counters &cnt) {
+    if (COUNT) { cnt.rays++; cnt.aabb++; }
+    T.best.t = 1e9f;
+    T.best.prim = -1;
+    T.best.u = T.best.v = 0.f;
+    T.sp = 0;
+    T.acc = 1e9f;
+    const NodeRec root = load_node(sc.node, 0);
+    T.a = root.a;
+    T.b = root.b;
+    float e;
+    return box_hit<false>(root.mn, root.mx, r, e);
+}
+
+// One round: descend to a leaf (or to a node with no child to visit), test the leaf's
+// triangles, then return up the frames until a far child is to be visited (false: more
+// rounds) or the stack is empty (true: T.best is final).
+template <bool COUNT, class Stack>
+__device__ __forceinline__ bool trav_round(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, Counters &cnt) {
+    uint32_t a = T.a, b = T.b;
+    float acc = T.acc;
+    int sp = T.sp;
+    bool leaf = true;
+    while (b < 3u) {
+        RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, a = 0);
+        NodeRec L, R;
+        load_pair(sc.node, a, L, R);
+        if (COUNT) cnt.aabb += 2;
+        const float ds = b == 0 ? r.d.x : (b == 1 ? r.d.y : r.d.z);
+        const bool lf = ds > 0;
+        NodeRec N, F;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            N.mn[k] = lf ? L.mn[k] : R.mn[k]; N.mx[k] = lf ? L.mx[k] : R.mx[k];
+            F.mn[k] = lf ? R.mn[k] : L.mn[k]; F.mx[k] = lf ? R.mx[k] : L.mx[k];
         }
-        if (leaf) {
-            const uint32_t kend = a + (b >> 2);
-            RT_CHECK(kend <= (uint32_t)sc.n_tris, 12, kend, a = kend);
-            for (uint32_t k = a; k < kend; ++k) {
-                V3 v0, U, V;
-                load_tri(sc.tri, (int)k, v0, U, V);
-                TriHit h;
-                if (COUNT) cnt.tri++;
-                if (tri_hit(v0, U, V, r, h)) {
-                    if (h.t < acc) acc = h.t;
-                    if (h.t < best.t) { best.t = h.t; best.u = h.u; best.v = h.v; best.prim = (int)k; }
-                }
+        N.a = lf ? L.a : R.a; N.b = lf ? L.b : R.b;
+        F.a = lf ? R.a : L.a; F.b = lf ? R.b : L.b;
+        float en, ef;
+        const bool hn = box_hit<false>(N.mn, N.mx, r, en);
+        const bool hf = box_hit<true>(F.mn, F.mx, r, ef);
+        if (hn) {
+            if (hf) {
+                RT_CHECK(sp < kStack, 11, sp, sp = 0);
+                stk.put(sp++, make_uint2((F.a << 10) | F.b, __float_as_uint(ef)));
+#ifdef RT_STACK_PROBE
+                RT_STACK_PROBE(sp);
+#endif
             }
+            a = N.a; b = N.b;
+        } else if (hf && !(ef > 1e9f)) {   // near missed: the node's local best is still 1e9
+            a = F.a; b = F.b;
+        } else {
+            leaf = false;
+            break;
         }
-        // return: merge subtree bests upwards until a far child is to be visited
-        for (;;) {
-            if (sp == 0) return;
-            const uint2 f = stk[--sp];
-            if (f.x == kFrameAcc) {
-                const float p = __uint_as_float(f.y);
-                acc = acc < p ? acc : p;
-                continue;
-            }
-            if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
-                stk[sp++] = make_uint2(kFrameAcc, __float_as_uint(acc));
-                a = f.x >> 10;
-                b = f.x & 1023u;
-                acc = 1e9f;
-                break;
+    }
+    if (leaf) {
+        const uint32_t kend = a + (b >> 2);
+        RT_CHECK(kend <= (uint32_t)sc.n_tris, 12, kend, a = kend);
+        for (uint32_t k = a; k < kend; ++k) {
+            V3 v0, U, V;
+            load_tri(sc.tri, (int)k, v0, U, V);
+            TriHit h;
+            if (COUNT) cnt.tri++;
+            if (tri_hit_bl(v0, U, V, r, h)) {
+                acc = h.t < acc ? h.t : acc;
+                if (h.t < T.best.t) { T.best.t = h.t; T.best.u = h.u; T.best.v = h.v; T.best.prim = (int)k; }
             }
         }
     }
+    // return: merge subtree bests upwards until a far child is to be visited
+    for (;;) {
+        if (sp == 0) {
+            T.sp = 0;
+            return true;
+        }
+        const uint2 f = stk.get(--sp);
+        if (f.x == kFrameAcc) {
+            const float p = __uint_as_float(f.y);
+            acc = acc < p ? acc : p;
+            continue;
+        }
+        if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
+            stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
+#ifdef RT_STACK_PROBE
+            RT_STACK_PROBE(sp);
+#endif
+            T.a = f.x >> 10;
+            T.b = f.x & 1023u;
+            T.acc = 1e9f;
+            T.sp = sp;
+            return false;
+        }
+    }
+}
+
+#ifdef __HIPCC__
+// Device stack: the first K entries in LDS (entry k of thread t at [k * 256 + t], so a
+// wave's 64 lanes hit consecutive 8-byte words), deeper entries in scratch.  K = 8 holds
+// 96% of all pushes on the sponza frame (tools: RT_STACK_PROBE histogram).
+template <int K>
+struct LdsStack {
+    uint2 *lds;   // &shared[threadIdx.x]
+    uint2 spill[kStack - K];
+    __device__ __forceinline__ void put(int i, uint2 v) {
+        if (i < K) lds[i * 256] = v;
+        else spill[i - K] = v;
+    }
+    __device__ __forceinline__ uint2 get(int i) const { return i < K ? lds[i * 256] : spill[i - K]; }
+};
+#endif
+
+// The whole closest-hit query (host tests; the device kernel interleaves rounds of many rays).
+template <bool COUNT>
+__device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const Ray &r, Hit &best, uint2 *stk, Counters &cnt) {
+    TravState T;
+    ArrayStack S{stk};
+    if (trav_start<COUNT>(sc, r, T, cnt))
+        while (!trav_round<COUNT>(sc, r, T, S, cnt)) {
+        }
+    best = T.best;
 }
 
 // Start sample s of slot i: jittered camera ray (scene.cpp:36-39); the first traversal
