@@ -37,6 +37,7 @@
 #include <geometry/primitive.h>
 #include <core/bvh.h>
 #include <utils/random.h>
+#include <render/canvas.h>
 // random.cpp's two file-statics (uniDist, normDist) become per-thread copies.
 #define static static thread_local
 #include <utils/random.cpp>
@@ -440,15 +441,61 @@ static int mode_samplers(int argc, char **argv) {
     return 0;
 }
 
+// finish <out.rtd> <out.ppm> W H spp: the frame finish of Scene::render (scene.cpp:54-64)
+// and Scene::draw_into (Canvas::write_to, canvas.h:76-89) on deterministic synthetic pixel
+// sums spanning zero, tiny, mid-range, saturating, negative and NaN/inf values.
+static int mode_finish(int argc, char **argv) {
+    if (argc < 7) throw std::runtime_error("finish out.rtd out.ppm W H spp");
+    const int W = std::atoi(argv[4]), H = std::atoi(argv[5]), spp = std::atoi(argv[6]);
+    std::vector<float> sums((size_t)W * H * 3);
+    uint32_t x = 12345u;
+    for (size_t k = 0; k < sums.size(); ++k) {
+        x = x * 1664525u + 1013904223u;
+        const float u = (float)(x >> 8) / 16777216.f;
+        const int kind = (int)(k % 11);
+        float v;
+        switch (kind) {
+            case 0: v = 0.f; break;
+            case 1: v = u * 1e-6f; break;
+            case 2: v = u * (float)spp * 4.f; break;
+            case 3: v = -u; break;
+            case 4: v = (k % 97 == 4) ? NAN : u * (float)spp; break;
+            case 5: v = (k % 89 == 5) ? INFINITY : u * (float)spp * 0.25f; break;
+            default: v = u * u * (float)spp * 1.5f; break;
+        }
+        sums[k] = v;
+    }
+    Canvas canvas({W, H});
+    const float normalizer = 1.f / (float)spp;
+    const float gamma_ = 1.f / 2.2f;   // scene.h:36
+    for (int j = 0; j < H; ++j)
+        for (int i = 0; i < W; ++i) {
+            const size_t o = 3 * ((size_t)j * W + i);
+            vector3f color{sums[o], sums[o + 1], sums[o + 2]};
+            color *= normalizer;
+            color = aces_tonemap(color);
+            color = pow(color, gamma_);
+            canvas.set({i, j}, normal_to_ch8bit(color));
+        }
+    canvas.write_to(argv[3]);
+    RtDump d(argv[2]);
+    d.put("sums", sums, {(uint64_t)H, (uint64_t)W, 3});
+    d.put("spp", std::vector<int32_t>{spp});
+    d.close();
+    std::printf("{\"mode\": \"finish\", \"width\": %d, \"height\": %d, \"spp\": %d}\n", W, H, spp);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     try {
-        if (argc < 2) throw std::runtime_error("usage: ref_harness sums|time|rays|dump|samplers ...");
+        if (argc < 2) throw std::runtime_error("usage: ref_harness sums|time|rays|dump|samplers|finish ...");
         std::string m = argv[1];
         if (m == "sums") return mode_sums(argc, argv);
         if (m == "time") return mode_time(argc, argv);
         if (m == "rays") return mode_rays(argc, argv);
         if (m == "dump") return mode_dump(argc, argv);
         if (m == "samplers") return mode_samplers(argc, argv);
+        if (m == "finish") return mode_finish(argc, argv);
         throw std::runtime_error("unknown mode " + m);
     } catch (const std::exception &e) {
         std::fprintf(stderr, "ref_harness: %s\n", e.what());

@@ -161,22 +161,23 @@ __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, 
     }
 }
 
-// Persistent traversal over the queue: every lane runs rounds of its own ray (rt_wavefront.h
-// trav_round); lanes whose ray finished take the next queued ray between rounds (one atomic
-// per wave), so a wave is never held by its slowest ray.
-constexpr int kLdsStack = 8;
+// Persistent traversal over the queue: each loop iteration advances every lane of a wave
+// by one unit of its own ray's traversal (rt_wavefront.h trav_step: one node pair or one
+// triangle).  Lanes whose ray is finished idle until kRefill of them are idle (or the wave
+// has nothing else to do), then take the next queued rays together (one atomic per wave).
+constexpr int kRefill = 16;
 template <bool COUNT>
 __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfState st, const int *queue,
                                                          const unsigned *count, unsigned *fetch, unsigned *next_count,
                                                          unsigned long long *counters) {
-    __shared__ uint2 lds_stack[kLdsStack * 256];
     const unsigned n = *count;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
         *next_count = 0;                                 // the shade kernel's output queue
     }
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    rtd::LdsStack<kLdsStack> S{&lds_stack[threadIdx.x], {}};
+    uint2 spill[rtd::kStack - rtd::kLdsStack];
+    rtd::LdsStack S{spill};
     const int lane = threadIdx.x & 63;
     int slot = -1;
     bool exhausted = false;
@@ -184,12 +185,13 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfStat
     rtd::TravState T;
     for (;;) {
         const unsigned long long m = __ballot(slot < 0);
-        if (m && !exhausted) {
+        const int idle = __popcll(m);
+        if (!exhausted && (idle >= kRefill || idle == 64)) {
             const int leader = __ffsll(m) - 1;
             unsigned base = 0;
-            if (lane == leader) base = atomicAdd(fetch, (unsigned)__popcll(m));
+            if (lane == leader) base = atomicAdd(fetch, (unsigned)idle);
             base = __shfl(base, leader, 64);
-            exhausted = base + (unsigned)__popcll(m) >= n;
+            exhausted = base + (unsigned)idle >= n;
             if (slot < 0) {
                 const unsigned q = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
                 if (q < n) {
@@ -205,7 +207,7 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfStat
                 }
             }
         }
-        if (slot >= 0 && rtd::trav_round<COUNT>(sc, r, T, S, cnt)) {
+        if (slot >= 0 && rtd::trav_step<COUNT>(sc, r, T, S, cnt)) {
             st.hprim[slot] = T.best.prim;
             st.ht[slot] = T.best.t;
             st.hu[slot] = T.best.u;

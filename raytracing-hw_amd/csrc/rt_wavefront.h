@@ -160,10 +160,13 @@ __device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriH
 }
 
 // Resumable traversal state of one ray.
+enum TravPhase : int { TP_NODE = 0, TP_LEAF = 1, TP_POP = 2 };
 struct TravState {
-    uint32_t a, b;   // node being entered: internal (b = split axis, a = left child) or leaf (b = 3 | n << 2, a = first)
+    uint32_t a, b;   // TP_NODE: internal node being entered (b = split axis, a = left child)
+    uint32_t k, kend;   // TP_LEAF: triangles still to test
     float acc;       // best t inside the subtree being traversed (the reference's local best)
     int sp;
+    int phase;
     Hit best;        // global winner so far (strict <, first of equal t wins)
 };
 
@@ -173,6 +176,16 @@ struct ArrayStack {
     __device__ __forceinline__ void put(int i, uint2 v) { p[i] = v; }
     __device__ __forceinline__ uint2 get(int i) const { return p[i]; }
 };
+
+// Enter a node given its (a, b) fields: internal -> TP_NODE, leaf -> TP_LEAF (an empty
+// leaf returns at once).
+__device__ __forceinline__ void trav_enter(TravState &T, uint32_t a, uint32_t b) {
+    T.a = a;
+    T.b = b;
+    T.k = a;
+    T.kend = a + (b >> 2);
+    T.phase = b < 3u ? TP_NODE : (T.kend > T.k ? TP_LEAF : TP_POP);
+}
 
 // BVH::intersect entry (bvh.cpp:239-243): counters, root box.  False = the ray misses the
 // scene (T.best says so).
@@ -185,23 +198,20 @@ __device__ __forceinline__ bool trav_start(const DevScene &sc, const Ray &r, Tra
     T.sp = 0;
     T.acc = 1e9f;
     const NodeRec root = load_node(sc.node, 0);
-    T.a = root.a;
-    T.b = root.b;
+    trav_enter(T, root.a, root.b);
     float e;
     return box_hit<false>(root.mn, root.mx, r, e);
 }
 
-// One round: descend to a leaf (or to a node with no child to visit), test the leaf's
-// triangles, then return up the frames until a far child is to be visited (false: more
-// rounds) or the stack is empty (true: T.best is final).
+// One unit of traversal work: the child pair of one internal node, or one leaf triangle,
+// followed (when the subtree is finished) by the return up the frames until a far child
+// is to be visited.  Returns true once the stack is empty (T.best is final).  A wave's
+// lanes each advance by one unit per call, whatever mix of units they are at.
 template <bool COUNT, class Stack>
-__device__ __forceinline__ bool trav_round(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, Counters &cnt) {
-    uint32_t a = T.a, b = T.b;
-    float acc = T.acc;
-    int sp = T.sp;
-    bool leaf = true;
-    while (b < 3u) {
-        RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, a = 0);
+__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, Counters &cnt) {
+    if (T.phase == TP_NODE) {
+        const uint32_t a = T.a, b = T.b;
+        RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, T.a = 0);
         NodeRec L, R;
         load_pair(sc.node, a, L, R);
         if (COUNT) cnt.aabb += 2;
@@ -218,85 +228,97 @@ __device__ __forceinline__ bool trav_round(const DevScene &sc, const Ray &r, Tra
         float en, ef;
         const bool hn = box_hit<false>(N.mn, N.mx, r, en);
         const bool hf = box_hit<true>(F.mn, F.mx, r, ef);
-        if (hn) {
-            if (hf) {
-                RT_CHECK(sp < kStack, 11, sp, sp = 0);
-                stk.put(sp++, make_uint2((F.a << 10) | F.b, __float_as_uint(ef)));
+        if (hn && hf) {
+            RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
+            stk.put(T.sp++, make_uint2((F.a << 10) | F.b, __float_as_uint(ef)));
+#ifdef RT_STACK_PROBE
+            RT_STACK_PROBE(T.sp);
+#endif
+        }
+        // near child; or, the near box missed, the far child unless its entry distance
+        // exceeds the node's local best (still 1e9); or return
+        const bool far_only = !hn && hf && !(ef > 1e9f);
+        if (hn || far_only) trav_enter(T, hn ? N.a : F.a, hn ? N.b : F.b);
+        else T.phase = TP_POP;
+    } else if (T.phase == TP_LEAF) {
+        const uint32_t k = T.k;
+        RT_CHECK(k < (uint32_t)sc.n_tris, 12, k, T.k = 0);
+        V3 v0, U, V;
+        load_tri(sc.tri, (int)k, v0, U, V);
+        TriHit h;
+        if (COUNT) cnt.tri++;
+        if (tri_hit_bl(v0, U, V, r, h)) {
+            T.acc = h.t < T.acc ? h.t : T.acc;
+            if (h.t < T.best.t) { T.best.t = h.t; T.best.u = h.u; T.best.v = h.v; T.best.prim = (int)k; }
+        }
+        T.k = k + 1;
+        if (T.k >= T.kend) T.phase = TP_POP;
+    }
+    if (T.phase == TP_POP) {
+        // return: merge subtree bests upwards until a far child is to be visited
+        float acc = T.acc;
+        int sp = T.sp;
+        for (;;) {
+            if (sp == 0) {
+                T.sp = 0;
+                T.acc = acc;
+                return true;
+            }
+            const uint2 f = stk.get(--sp);
+            if (f.x == kFrameAcc) {
+                const float p = __uint_as_float(f.y);
+                acc = acc < p ? acc : p;
+                continue;
+            }
+            if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
+                stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
 #ifdef RT_STACK_PROBE
                 RT_STACK_PROBE(sp);
 #endif
-            }
-            a = N.a; b = N.b;
-        } else if (hf && !(ef > 1e9f)) {   // near missed: the node's local best is still 1e9
-            a = F.a; b = F.b;
-        } else {
-            leaf = false;
-            break;
-        }
-    }
-    if (leaf) {
-        const uint32_t kend = a + (b >> 2);
-        RT_CHECK(kend <= (uint32_t)sc.n_tris, 12, kend, a = kend);
-        for (uint32_t k = a; k < kend; ++k) {
-            V3 v0, U, V;
-            load_tri(sc.tri, (int)k, v0, U, V);
-            TriHit h;
-            if (COUNT) cnt.tri++;
-            if (tri_hit_bl(v0, U, V, r, h)) {
-                acc = h.t < acc ? h.t : acc;
-                if (h.t < T.best.t) { T.best.t = h.t; T.best.u = h.u; T.best.v = h.v; T.best.prim = (int)k; }
+                T.sp = sp;
+                T.acc = 1e9f;
+                trav_enter(T, f.x >> 10, f.x & 1023u);
+                return false;
             }
         }
     }
-    // return: merge subtree bests upwards until a far child is to be visited
-    for (;;) {
-        if (sp == 0) {
-            T.sp = 0;
-            return true;
-        }
-        const uint2 f = stk.get(--sp);
-        if (f.x == kFrameAcc) {
-            const float p = __uint_as_float(f.y);
-            acc = acc < p ? acc : p;
-            continue;
-        }
-        if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
-            stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
-#ifdef RT_STACK_PROBE
-            RT_STACK_PROBE(sp);
-#endif
-            T.a = f.x >> 10;
-            T.b = f.x & 1023u;
-            T.acc = 1e9f;
-            T.sp = sp;
-            return false;
-        }
-    }
+    return false;
 }
 
 #ifdef __HIPCC__
 // Device stack: the first K entries in LDS (entry k of thread t at [k * 256 + t], so a
 // wave's 64 lanes hit consecutive 8-byte words), deeper entries in scratch.  K = 8 holds
 // 96% of all pushes on the sponza frame (tools: RT_STACK_PROBE histogram).
-template <int K>
+constexpr int kLdsStack = 8;
+__shared__ uint2 wf_lds_stack[kLdsStack * 256];   // blocks of 256 threads
 struct LdsStack {
-    uint2 *lds;   // &shared[threadIdx.x]
-    uint2 spill[kStack - K];
+    uint2 *spill;   // this thread's private overflow array (scratch), kStack - kLdsStack entries
     __device__ __forceinline__ void put(int i, uint2 v) {
-        if (i < K) lds[i * 256] = v;
-        else spill[i - K] = v;
+        if (i < kLdsStack) wf_lds_stack[i * 256 + threadIdx.x] = v;
+        else spill[i - kLdsStack] = v;
     }
-    __device__ __forceinline__ uint2 get(int i) const { return i < K ? lds[i * 256] : spill[i - K]; }
+    __device__ __forceinline__ uint2 get(int i) const {
+        uint2 v;
+        if (i < kLdsStack) {
+            v = wf_lds_stack[i * 256 + threadIdx.x];
+        } else {
+            v = spill[i - kLdsStack];
+            // keeps the two loads apart: merged, they become one flat load through a
+            // selected pointer instead of a ds_read
+            asm volatile("" : "+v"(v.x), "+v"(v.y));
+        }
+        return v;
+    }
 };
 #endif
 
-// The whole closest-hit query (host tests; the device kernel interleaves rounds of many rays).
+// The whole closest-hit query (host tests; the device kernel interleaves the steps of many rays).
 template <bool COUNT>
 __device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const Ray &r, Hit &best, uint2 *stk, Counters &cnt) {
     TravState T;
     ArrayStack S{stk};
     if (trav_start<COUNT>(sc, r, T, cnt))
-        while (!trav_round<COUNT>(sc, r, T, S, cnt)) {
+        while (!trav_step<COUNT>(sc, r, T, S, cnt)) {
         }
     best = T.best;
 }

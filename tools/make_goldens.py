@@ -73,11 +73,25 @@ def row_hash(sums):
     return h
 
 
+def finish_golden(meta):
+    """Frame finish (tonemap + 8-bit + PPM) of the reference on synthetic sums."""
+    ppm = os.path.join(GOLD, "finish_37x23x16.ppm")
+    meta["finish"] = harness("finish", os.path.join(GOLD, "finish_37x23x16.rtd"), ppm, 37, 23, 16)
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
     os.makedirs(GOLD, exist_ok=True)
+    if "--finish-only" in sys.argv:
+        path = os.path.join(GOLD, "golden_meta.json")
+        meta = json.load(open(path))
+        finish_golden(meta)
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        return
     meta = {}
+    finish_golden(meta)
     for name in SCENES:
         sdir = os.path.join(GOLD, "scenes", name)
         if os.path.isdir(sdir):
