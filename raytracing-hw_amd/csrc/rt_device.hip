@@ -13,6 +13,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <cstdlib>
 
 #include "rt_path.h"
 #include "rt_wave.h"
@@ -34,9 +35,14 @@ struct rt_device_scene {
     long long wf_cap = 0;
     int wf_D = 0;
     rtd::WfState wf{};
-    int *wf_queue[2] = {nullptr, nullptr};
+    float4 *wf_queue[2] = {nullptr, nullptr};
+    float4 *wf_hits = nullptr;
     unsigned *wf_count = nullptr;  // [2]
     unsigned *wf_host_count = nullptr;  // pinned
+    // tuning (RT_WF_REFILL, RT_WF_CHUNK, RT_WF_EXTEND_BLOCKS_PER_CU environment overrides, read at upload)
+    int wf_refill = 8;
+    int wf_chunk = 64;
+    int wf_ext_bpc = 0;   // 0 = as many as fit
 };
 
 #define HIP_TRY(expr)                                                                          \
@@ -151,25 +157,29 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
 
 // ------------------------------------------------------------------------ wavefront
 // (rt_wavefront.h) init -> { extend ; shade } until every slot has finished its samples.
-__global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int *queue,
-                                                       unsigned *count) {
+__global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, rtd::WfState st, float4 *qout,
+                                                       unsigned *cout) {
     for (long long base = (long long)blockIdx.x * blockDim.x; base < st.n; base += (long long)gridDim.x * blockDim.x) {
         const long long i = base + threadIdx.x;
         const bool valid = i < st.n;
-        if (valid) rtd::wf_init_slot(sc, g, st, i);
-        rtd::queue_push(valid, (int)i, queue, count);
+        rtd::Ray r;
+        if (valid) r = rtd::wf_init_slot(sc, g, st, i);
+        const unsigned p = rtd::queue_slot(valid, cout);
+        if (valid) rtd::store_qray(qout, p, (int)i, r);
     }
 }
 
 // Persistent traversal over the queue: each loop iteration advances every lane of a wave
 // by one unit of its own ray's traversal (rt_wavefront.h trav_step: one node pair or one
-// triangle).  Lanes whose ray is finished idle until kRefill of them are idle (or the wave
-// has nothing else to do), then take the next queued rays together (one atomic per wave).
-constexpr int kRefill = 16;
+// triangle).  Lanes whose ray is finished idle until `refill` of them are idle (or the
+// wave has nothing else to do), then take the next rays of the wave's current chunk of the
+// queue; a wave claims a new chunk of `chunk` entries with one atomic when its chunk runs
+// out (a single shared counter hit by every refill serialises all waves on one address).
+// The rays sit in the queue entries: one coalesced load each.
 template <bool COUNT>
-__global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfState st, const int *queue,
-                                                         const unsigned *count, unsigned *fetch, unsigned *next_count,
-                                                         unsigned long long *counters) {
+__global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float4 *qin, const unsigned *count,
+                                                         float4 *hits, unsigned *fetch, unsigned *next_count,
+                                                         unsigned long long *counters, int refill, unsigned chunk) {
     const unsigned n = *count;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
@@ -179,59 +189,71 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, rtd::WfStat
     uint2 spill[rtd::kStack - rtd::kLdsStack];
     rtd::LdsStack S{spill};
     const int lane = threadIdx.x & 63;
-    int slot = -1;
-    bool exhausted = false;
+    unsigned q = 0, lo = 0, hi = 0;   // [lo, hi): the wave's unclaimed part of its chunk
+    bool busy = false, exhausted = false;
     rtd::Ray r;
     rtd::TravState T;
     for (;;) {
-        const unsigned long long m = __ballot(slot < 0);
-        const int idle = __popcll(m);
-        if (!exhausted && (idle >= kRefill || idle == 64)) {
-            const int leader = __ffsll(m) - 1;
-            unsigned base = 0;
-            if (lane == leader) base = atomicAdd(fetch, (unsigned)idle);
-            base = __shfl(base, leader, 64);
-            exhausted = base + (unsigned)idle >= n;
-            if (slot < 0) {
-                const unsigned q = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                if (q < n) {
-                    slot = queue[q];
-                    r = rtd::load_ray(st, slot);
-                    if (!rtd::trav_start<COUNT>(sc, r, T, cnt)) {
-                        st.hprim[slot] = -1;   // misses the scene box
-                        st.ht[slot] = T.best.t;
-                        st.hu[slot] = 0.f;
-                        st.hv[slot] = 0.f;
-                        slot = -1;
+        const unsigned long long m = __ballot(!busy);
+        const unsigned idle = (unsigned)__popcll(m);
+        if (!exhausted && (idle >= (unsigned)refill || idle == 64)) {
+            const unsigned rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            unsigned got = 0, mine = 0xffffffffu;
+            while (got < idle) {
+                if (lo >= hi) {
+                    unsigned b = 0;
+                    if (lane == 0) b = atomicAdd(fetch, chunk);
+                    b = __shfl(b, 0, 64);
+                    if (b >= n) {
+                        exhausted = true;
+                        break;
                     }
+                    lo = b;
+                    hi = b + chunk < n ? b + chunk : n;
                 }
+                const unsigned k = hi - lo < idle - got ? hi - lo : idle - got;
+                if (!busy && rank >= got && rank < got + k) mine = lo + (rank - got);
+                lo += k;
+                got += k;
+            }
+            if (mine != 0xffffffffu) {
+                q = mine;
+                int slot;
+                r = rtd::load_qray(qin, q, slot);
+                busy = rtd::trav_start<COUNT>(sc, r, T, cnt);
+                if (!busy) rtd::store_hit(hits, q, T.best);   // misses the scene box
             }
         }
-        if (slot >= 0 && rtd::trav_step<COUNT>(sc, r, T, S, cnt)) {
-            st.hprim[slot] = T.best.prim;
-            st.ht[slot] = T.best.t;
-            st.hu[slot] = T.best.u;
-            st.hv[slot] = T.best.v;
-            slot = -1;
+        if (busy && rtd::trav_step<COUNT>(sc, r, T, S, cnt)) {
+            rtd::store_hit(hits, q, T.best);
+            busy = false;
         }
-        if (exhausted && !__any(slot >= 0)) break;
+        if (exhausted && !__any(busy)) break;
     }
     rtd::counters_flush<COUNT>(cnt, counters);
 }
 
 template <bool COUNT>
 __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp,
-                                                        const int *qin, const unsigned *cin, int *qout, unsigned *cout,
-                                                        unsigned *fetch, float *out, unsigned long long *counters) {
+                                                        const float4 *qin, const unsigned *cin, const float4 *hits,
+                                                        float4 *qout, unsigned *cout, unsigned *fetch, float *out,
+                                                        unsigned long long *counters) {
     const unsigned n = *cin;
     if (blockIdx.x == 0 && threadIdx.x == 0) *fetch = 0;   // the next extend launch's ray counter
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     for (unsigned base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const unsigned q = base + threadIdx.x;
         const bool valid = q < n;
-        const int i = valid ? qin[q] : 0;
-        const bool next = valid && rtd::wf_shade_slot<COUNT>(sc, g, st, spp, i, out, cnt);
-        rtd::queue_push(next, i, qout, cout);
+        int slot = 0;
+        bool next = false;
+        rtd::Ray r;
+        if (valid) {
+            r = rtd::load_qray(qin, q, slot);
+            const rtd::Hit h = rtd::load_hit(hits, q);
+            next = rtd::wf_shade_slot<COUNT>(sc, g, st, spp, slot, r, h, out, cnt);
+        }
+        const unsigned p = rtd::queue_slot(next, cout);
+        if (next) rtd::store_qray(qout, p, slot, r);
     }
     rtd::counters_flush<COUNT>(cnt, counters);
 }
@@ -311,6 +333,9 @@ int ensure_device_scene(rt_scene *s, int device) {
         return rt_fail(RT_ERR_DEVICE, std::string("scene upload: ") + hipGetErrorString(e));
     }
     d->cu_count = prop.multiProcessorCount;
+    if (const char *e = std::getenv("RT_WF_REFILL")) d->wf_refill = std::max(1, std::min(64, std::atoi(e)));
+    if (const char *e = std::getenv("RT_WF_CHUNK")) d->wf_chunk = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("RT_WF_EXTEND_BLOCKS_PER_CU")) d->wf_ext_bpc = std::max(0, std::atoi(e));
     uint8_t *b = (uint8_t *)d->buf;
     DevScene &ds = d->ds;
     ds.tri = (const float4 *)(b + o_tri);
@@ -349,37 +374,35 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     d->wf_count = nullptr;
     d->wf_host_count = nullptr;
     const long long cap = ((n + 255) / 256) * 256;
-    const int planes_f = 6 + 3 + 1 + 3 + 9 * D;   // ray, hit t/u/v, rng_saved, sums, records
-    const int planes_i = 1 + 1 + 1 + 2;           // hprim, rng_x, meta, queues
-    const size_t bytes = (size_t)cap * 4 * (size_t)(planes_f + planes_i);
+    const int planes = 2 + 1 + 3 + 9 * D      // rng, meta, sums, vertex records (per slot)
+                       + 2 * 8 + 4;           // two ray queues (32 B / entry), hits (16 B / entry)
+    const size_t bytes = (size_t)cap * 4 * (size_t)planes;
     HIP_TRY(hipMalloc(&d->wf_buf, bytes));
     HIP_TRY(hipMalloc((void **)&d->wf_count, 64));
     HIP_TRY(hipHostMalloc((void **)&d->wf_host_count, 64, hipHostMallocDefault));
     float *f = (float *)d->wf_buf;
-    auto take = [&](void) { float *p = f; f += cap; return p; };
+    auto take = [&](int k) { float *p = f; f += (size_t)cap * k; return p; };
     rtd::WfState &w = d->wf;
     w.n = n;
     w.D = D;
-    w.ox = take(); w.oy = take(); w.oz = take(); w.dx = take(); w.dy = take(); w.dz = take();
-    w.ht = take(); w.hu = take(); w.hv = take();
-    w.rng_saved = take();
-    w.sx = take(); w.sy = take(); w.sz = take();
-    w.rec = f;
-    f += (size_t)cap * 9 * D;
-    w.hprim = (int *)take();
-    w.rng_x = (uint32_t *)take();
-    w.meta = (uint32_t *)take();
-    d->wf_queue[0] = (int *)take();
-    d->wf_queue[1] = (int *)take();
+    d->wf_queue[0] = (float4 *)take(8);   // 16-B aligned: cap is a multiple of 256
+    d->wf_queue[1] = (float4 *)take(8);
+    d->wf_hits = (float4 *)take(4);
+    w.rng_x = (uint32_t *)take(1);
+    w.rng_saved = take(1);
+    w.meta = (uint32_t *)take(1);
+    w.sx = take(1); w.sy = take(1); w.sz = take(1);
+    w.rec = take(9 * D);
     d->wf_cap = cap;
     d->wf_D = D;
     return RT_OK;
 }
 
 template <class K>
-unsigned persistent_blocks(rt_device_scene *d, K kernel, long long work) {
+unsigned persistent_blocks(rt_device_scene *d, K kernel, long long work, int cap_per_cu = 0) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (cap_per_cu > 0 && per_cu > cap_per_cu) per_cu = cap_per_cu;
     long long need = (work + 255) / 256;
     long long b = std::min<long long>(need, (long long)d->cu_count * per_cu);
     return (unsigned)std::max<long long>(b, 1);
@@ -431,8 +454,8 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     const unsigned init_blocks = (unsigned)std::min<long long>((g.n_pixels + 255) / 256, (long long)d->cu_count * 8);
     hipLaunchKernelGGL(wf_init_kernel, dim3(init_blocks), dim3(256), 0, stream, d->ds, g, w, d->wf_queue[0], &d->wf_count[0]);
     HIP_TRY(hipGetLastError());
-    const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, g.n_pixels)
-                                      : persistent_blocks(d, wf_extend_kernel<false>, g.n_pixels);
+    const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, g.n_pixels, d->wf_ext_bpc)
+                                      : persistent_blocks(d, wf_extend_kernel<false>, g.n_pixels, d->wf_ext_bpc);
     const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true>, g.n_pixels)
                                      : persistent_blocks(d, wf_shade_kernel<false>, g.n_pixels);
     const long long max_iter = (long long)spp * depth + 16;
@@ -440,12 +463,12 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     for (long long it = 0;; ++it) {
         if (it > max_iter) return rt_fail(RT_ERR_DEVICE, "wavefront path did not drain (internal error)");
         HIP_TRY(timer.mark(0, stream));
-        if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], &d->wf_count[2], &d->wf_count[1 - cur], d->counters);
-        else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, w, d->wf_queue[cur], &d->wf_count[cur], &d->wf_count[2], &d->wf_count[1 - cur], d->counters);
+        if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, &d->wf_count[2], &d->wf_count[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
+        else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, &d->wf_count[2], &d->wf_count[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
         HIP_TRY(timer.mark(0, stream));
         HIP_TRY(timer.mark(1, stream));
-        if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
-        else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
+        if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
+        else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
         HIP_TRY(timer.mark(1, stream));
         HIP_TRY(hipGetLastError());
         cur = 1 - cur;

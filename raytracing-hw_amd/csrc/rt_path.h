@@ -22,6 +22,8 @@ inline uint2 make_uint2(uint32_t a, uint32_t b) { return {a, b}; }
 inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 inline int __float_as_int(float f) { int u; std::memcpy(&u, &f, 4); return u; }
+inline float __int_as_float(int u) { float f; std::memcpy(&f, &u, 4); return f; }
+inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
 using std::isnan;
 #endif
 

@@ -21,9 +21,6 @@ namespace rtd {
 struct WfState {
     long long n;      // path slots (= pixels of the shard)
     int D;            // vertex records per slot (= ray_depth)
-    float *ox, *oy, *oz, *dx, *dy, *dz;   // current ray (origin, normalised direction)
-    float *ht, *hu, *hv;                  // closest hit of the current ray
-    int *hprim;                           // -1 = miss
     uint32_t *rng_x;
     float *rng_saved;
     uint32_t *meta;                       // s (bits 0-19), power (20-23), nv (24-27), saved flag (28)
@@ -31,21 +28,47 @@ struct WfState {
     float *rec;                           // 9 * D planes of n floats (SoARec)
 };
 
+// Queues hold the rays themselves, 32 bytes per entry, so a kernel reading entry q gets its
+// ray with two coalesced 16-byte loads:  [2q] = (origin, slot bits), [2q + 1] = (dir, 0).
+// Hits are written by queue position, 16 bytes: (t, u, v, prim bits).
+__device__ __forceinline__ void store_qray(float4 *q, unsigned p, int slot, const Ray &r) {
+    q[2 * (size_t)p] = make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(slot));
+    q[2 * (size_t)p + 1] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
+}
+// Ray::Ray's state from the stored fields: inv_direction = {1,1,1} / direction (exact).
+__device__ __forceinline__ Ray load_qray(const float4 *q, unsigned p, int &slot) {
+    const float4 a = q[2 * (size_t)p], b = q[2 * (size_t)p + 1];
+    Ray r;
+    r.o = V3{a.x, a.y, a.z};
+    r.d = V3{b.x, b.y, b.z};
+    r.inv = rtv::divv(V3{1.f, 1.f, 1.f}, r.d);
+    slot = __float_as_int(a.w);
+    return r;
+}
+__device__ __forceinline__ void store_hit(float4 *hits, unsigned p, const Hit &h) {
+    hits[p] = make_float4(h.t, h.u, h.v, __int_as_float(h.prim));
+}
+__device__ __forceinline__ Hit load_hit(const float4 *hits, unsigned p) {
+    const float4 a = hits[p];
+    return Hit{a.x, a.y, a.z, __float_as_int(a.w)};
+}
+
 __device__ __forceinline__ uint32_t meta_pack(int s, int power, int nv, uint32_t saved) {
     return (uint32_t)s | ((uint32_t)power << 20) | ((uint32_t)nv << 24) | (saved << 28);
 }
 
 #ifdef __HIPCC__
-// Appends `slot` to a queue when `want`: one atomic per wave, lanes keep their order.
-__device__ __forceinline__ void queue_push(bool want, int slot, int *queue, unsigned *count) {
+// Position of this lane's entry in a queue when `want` (else undefined): one atomic per
+// wave, lanes keep their order.
+__device__ __forceinline__ unsigned queue_slot(bool want, unsigned *count) {
     const unsigned long long m = __ballot(want);
-    if (!m) return;
+    if (!m) return 0;
     const int lane = threadIdx.x & 63;
     const int leader = __ffsll((unsigned long long)m) - 1;
     unsigned base = 0;
     if (lane == leader) base = atomicAdd(count, (unsigned)__popcll(m));
     base = __shfl(base, leader, 64);
-    if (want) queue[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
+    return base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
 }
 
 template <bool COUNT>
@@ -60,19 +83,6 @@ __device__ __forceinline__ void counters_flush(const Counters &c, unsigned long 
     }
 }
 #endif
-
-__device__ __forceinline__ void store_ray(const WfState &st, long long i, const Ray &r) {
-    st.ox[i] = r.o.x; st.oy[i] = r.o.y; st.oz[i] = r.o.z;
-    st.dx[i] = r.d.x; st.dy[i] = r.d.y; st.dz[i] = r.d.z;
-}
-// Ray::Ray's state from the stored fields: inv_direction = {1,1,1} / direction (exact).
-__device__ __forceinline__ Ray load_ray(const WfState &st, long long i) {
-    Ray r;
-    r.o = V3{st.ox[i], st.oy[i], st.oz[i]};
-    r.d = V3{st.dx[i], st.dy[i], st.dz[i]};
-    r.inv = rtv::divv(V3{1.f, 1.f, 1.f}, r.d);
-    return r;
-}
 
 // ---------------------------------------------------------------- extend traversal
 // BVH::intersect (bvh.cpp:177-243) for the extend kernel.  Same visits, same counters and
@@ -338,45 +348,31 @@ __device__ __forceinline__ Ray start_sample(const DevScene &sc, const ShardGeom 
 // test harness (tests/native/kernel_host.cpp) runs the same functions with a host queue.
 
 // wf_init: seed slot i's RNG from its pixel (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1)
-// and start its first sample.
-__device__ __forceinline__ void wf_init_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, long long i) {
+// and start its first sample; returns the camera ray.
+__device__ __forceinline__ Ray wf_init_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, long long i) {
     const int k = (int)(i / g.width), px = (int)(i % g.width), py = shard_row(g, k);
     const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
     Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
     int power = 0;
     const Ray r = start_sample(sc, g, i, rng, power);
-    store_ray(st, i, r);
     st.sx[i] = st.sy[i] = st.sz[i] = 0.f;
     st.rng_x[i] = rng.x;
     st.rng_saved[i] = rng.saved;
     st.meta[i] = meta_pack(0, power, 0, rng.saved_avail);
+    return r;
 }
 
-// wf_extend: closest hit of slot i's current ray.
-template <bool COUNT>
-__device__ __forceinline__ void wf_extend_slot(const DevScene &sc, const WfState &st, long long i, uint2 *stk,
-                                               Counters &cnt) {
-    const Ray r = load_ray(st, i);
-    Hit h;
-    closest_hit_wf<COUNT>(sc, r, h, stk, cnt);
-    st.hprim[i] = h.prim;
-    st.ht[i] = h.t;
-    st.hu[i] = h.u;
-    st.hv[i] = h.v;
-}
-
-// wf_shade: one vertex of scene.cpp:85-154 for slot i, then bounce (true: the slot has a
-// new ray to extend) or end the path: fold it, add it to the pixel sum (scene.cpp:41-42)
-// and start the next sample, or write the pixel after the last one (false).
+// wf_shade: one vertex of scene.cpp:85-154 for slot i (ray r, its closest hit h), then
+// bounce (true: r is the slot's next ray to extend) or end the path: fold it, add it to the
+// pixel sum (scene.cpp:41-42) and start the next sample (true, r = its camera ray), or
+// write the pixel after the last sample (false).
 template <bool COUNT>
 __device__ __forceinline__ bool wf_shade_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, int spp,
-                                              long long i, float *out, Counters &cnt) {
-    Ray r = load_ray(st, i);
+                                              long long i, Ray &r, const Hit &h, float *out, Counters &cnt) {
     const uint32_t meta = st.meta[i];
     int s = (int)(meta & 0xfffffu), power = (int)((meta >> 20) & 15u), nv = (int)((meta >> 24) & 15u);
     Rng rng{st.rng_x[i], (meta >> 28) & 1u, st.rng_saved[i]};
     SoARec P{st.rec, st.n, i, st.D};
-    const Hit h{st.ht[i], st.hu[i], st.hv[i], st.hprim[i]};
     bool next = false;
     // the recursion continues with the bounce ray while calls remain (scene.cpp:72-75)
     if (h.prim >= 0 && h.t < sc.max_distance && shade_hit<COUNT>(sc, r, h, rng, cnt, P, nv) && power > 0) {
@@ -399,7 +395,6 @@ __device__ __forceinline__ bool wf_shade_slot(const DevScene &sc, const ShardGeo
             next = true;
         }
     }
-    if (next) store_ray(st, i, r);
     st.meta[i] = meta_pack(s, power, nv, rng.saved_avail);
     st.rng_x[i] = rng.x;
     st.rng_saved[i] = rng.saved;

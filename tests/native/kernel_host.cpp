@@ -129,7 +129,7 @@ extern "C" int kh_render_wave(const rt_scene_view *v, int spp, int rank, int wor
 }
 
 // Emulates the wavefront path (wf_init / wf_extend / wf_shade in rt_device.hip) on the host:
-// the same rt_wavefront.h slot functions over SoA state, driven by a host queue.
+// the same rt_wavefront.h slot functions and queue records, driven by a host queue.
 extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world, int row_block, float *out,
                             uint64_t *cnt_out, int64_t *iterations) {
     rtd::DevScene sc = make(v);
@@ -141,31 +141,42 @@ extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world
     const long long n = (long long)rows * v->width;
     rtd::ShardGeom g{v->width, rank, world, row_block, n};
     const int D = v->ray_depth;
-    std::vector<float> f((size_t)n * (13 + 9 * D));
-    std::vector<uint32_t> u((size_t)n * 3);
+    std::vector<float> f((size_t)n * (5 + 9 * D));
+    std::vector<uint32_t> u((size_t)n * 2);
     rtd::WfState st{};
     st.n = n;
     st.D = D;
-    float *fp = f.data();
-    float **planes[] = {&st.ox, &st.oy, &st.oz, &st.dx, &st.dy, &st.dz, &st.ht, &st.hu, &st.hv, &st.rng_saved,
-                        &st.sx, &st.sy, &st.sz};
-    for (float **pp : planes) { *pp = fp; fp += n; }
-    st.rec = fp;
-    st.hprim = (int *)u.data();
-    st.rng_x = u.data() + n;
-    st.meta = u.data() + 2 * n;
-    std::vector<int> q, q2;
-    for (long long i = 0; i < n; ++i) { rtd::wf_init_slot(sc, g, st, i); q.push_back((int)i); }
+    st.rng_saved = f.data();
+    st.sx = f.data() + n;
+    st.sy = f.data() + 2 * n;
+    st.sz = f.data() + 3 * n;
+    st.rec = f.data() + 5 * n;
+    st.rng_x = u.data();
+    st.meta = u.data() + n;
+    std::vector<float4> q((size_t)2 * n), q2((size_t)2 * n), hits((size_t)n);
+    unsigned cnt_q = 0;
+    for (long long i = 0; i < n; ++i) rtd::store_qray(q.data(), cnt_q++, (int)i, rtd::wf_init_slot(sc, g, st, i));
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 stk[rtd::kStack];
     int64_t it = 0;
-    while (!q.empty()) {
+    while (cnt_q > 0) {
         if (++it > (int64_t)spp * D + 16) return -1;
-        for (int i : q) rtd::wf_extend_slot<true>(sc, st, i, stk, cnt);
-        q2.clear();
-        for (int i : q)
-            if (rtd::wf_shade_slot<true>(sc, g, st, spp, i, out, cnt)) q2.push_back(i);
+        for (unsigned p = 0; p < cnt_q; ++p) {   // extend
+            int slot;
+            const rtd::Ray r = rtd::load_qray(q.data(), p, slot);
+            rtd::Hit h;
+            rtd::closest_hit_wf<true>(sc, r, h, stk, cnt);
+            rtd::store_hit(hits.data(), p, h);
+        }
+        unsigned cnt_q2 = 0;
+        for (unsigned p = 0; p < cnt_q; ++p) {   // shade
+            int slot;
+            rtd::Ray r = rtd::load_qray(q.data(), p, slot);
+            const rtd::Hit h = rtd::load_hit(hits.data(), p);
+            if (rtd::wf_shade_slot<true>(sc, g, st, spp, slot, r, h, out, cnt)) rtd::store_qray(q2.data(), cnt_q2++, slot, r);
+        }
         q.swap(q2);
+        cnt_q = cnt_q2;
     }
     uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
     std::memcpy(cnt_out, c, sizeof c);
