@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, 
         rtd::Ray r;
         if (valid) r = rtd::wf_init_slot(sc, g, st, i);
         const unsigned p = rtd::queue_slot(valid, cout);
-        if (valid) rtd::store_qray(qout, p, (int)i, r);
+        if (valid) rtd::store_qray(sc, qout, p, (int)i, r);
     }
 }
 
@@ -189,6 +189,7 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
     uint2 spill[rtd::kStack - rtd::kLdsStack];
     rtd::LdsStack S{spill};
     const int lane = threadIdx.x & 63;
+    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
     unsigned q = 0, lo = 0, hi = 0;   // [lo, hi): the wave's unclaimed part of its chunk
     bool busy = false, exhausted = false;
     rtd::Ray r;
@@ -218,9 +219,9 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
             }
             if (mine != 0xffffffffu) {
                 q = mine;
-                int slot;
-                r = rtd::load_qray(qin, q, slot);
-                busy = rtd::trav_start<COUNT>(sc, r, T, cnt);
+                uint32_t bits;
+                r = rtd::load_qray_trav(qin, q, bits);
+                busy = rtd::trav_start<COUNT>(bits, root.a, root.b, T, cnt);
                 if (!busy) rtd::store_hit(hits, q, T.best);   // misses the scene box
             }
         }
@@ -253,7 +254,7 @@ __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc, ShardGeom g,
             next = rtd::wf_shade_slot<COUNT>(sc, g, st, spp, slot, r, h, out, cnt);
         }
         const unsigned p = rtd::queue_slot(next, cout);
-        if (next) rtd::store_qray(qout, p, slot, r);
+        if (next) rtd::store_qray(sc, qout, p, slot, r);
     }
     rtd::counters_flush<COUNT>(cnt, counters);
 }
@@ -375,7 +376,7 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     d->wf_host_count = nullptr;
     const long long cap = ((n + 255) / 256) * 256;
     const int planes = 2 + 1 + 3 + 9 * D      // rng, meta, sums, vertex records (per slot)
-                       + 2 * 8 + 4;           // two ray queues (32 B / entry), hits (16 B / entry)
+                       + 2 * 4 * rtd::kQRec + 4;   // two ray queues (48 B / entry), hits (16 B / entry)
     const size_t bytes = (size_t)cap * 4 * (size_t)planes;
     HIP_TRY(hipMalloc(&d->wf_buf, bytes));
     HIP_TRY(hipMalloc((void **)&d->wf_count, 64));
@@ -385,8 +386,8 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     rtd::WfState &w = d->wf;
     w.n = n;
     w.D = D;
-    d->wf_queue[0] = (float4 *)take(8);   // 16-B aligned: cap is a multiple of 256
-    d->wf_queue[1] = (float4 *)take(8);
+    d->wf_queue[0] = (float4 *)take(4 * rtd::kQRec);   // 16-B aligned: cap is a multiple of 256
+    d->wf_queue[1] = (float4 *)take(4 * rtd::kQRec);
     d->wf_hits = (float4 *)take(4);
     w.rng_x = (uint32_t *)take(1);
     w.rng_saved = take(1);

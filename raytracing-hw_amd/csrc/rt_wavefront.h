@@ -28,23 +28,6 @@ struct WfState {
     float *rec;                           // 9 * D planes of n floats (SoARec)
 };
 
-// Queues hold the rays themselves, 32 bytes per entry, so a kernel reading entry q gets its
-// ray with two coalesced 16-byte loads:  [2q] = (origin, slot bits), [2q + 1] = (dir, 0).
-// Hits are written by queue position, 16 bytes: (t, u, v, prim bits).
-__device__ __forceinline__ void store_qray(float4 *q, unsigned p, int slot, const Ray &r) {
-    q[2 * (size_t)p] = make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(slot));
-    q[2 * (size_t)p + 1] = make_float4(r.d.x, r.d.y, r.d.z, 0.f);
-}
-// Ray::Ray's state from the stored fields: inv_direction = {1,1,1} / direction (exact).
-__device__ __forceinline__ Ray load_qray(const float4 *q, unsigned p, int &slot) {
-    const float4 a = q[2 * (size_t)p], b = q[2 * (size_t)p + 1];
-    Ray r;
-    r.o = V3{a.x, a.y, a.z};
-    r.d = V3{b.x, b.y, b.z};
-    r.inv = rtv::divv(V3{1.f, 1.f, 1.f}, r.d);
-    slot = __float_as_int(a.w);
-    return r;
-}
 __device__ __forceinline__ void store_hit(float4 *hits, unsigned p, const Hit &h) {
     hits[p] = make_float4(h.t, h.u, h.v, __int_as_float(h.prim));
 }
@@ -120,30 +103,31 @@ __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], co
     const float o[3] = {r.o.x, r.o.y, r.o.z};
     const float d[3] = {r.d.x, r.d.y, r.d.z};
     const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+    // (bitwise & | on the conditions: short-circuit && || would be compiled to branches)
     bool inside = true;
     bool mid[3];
     float cand[3], maxT[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const bool lo = o[i] < mn[i];
-        const bool hi = !lo && o[i] > mx[i];
-        mid[i] = !lo && !hi;
+        const bool hi = !lo & (o[i] > mx[i]);
+        mid[i] = !lo & !hi;
         cand[i] = lo ? mn[i] : (hi ? mx[i] : 0.f);
-        inside = inside && mid[i];
-        maxT[i] = (!mid[i] && d[i] != 0.f) ? (cand[i] - o[i]) * inv[i] : -1.f;
+        inside = inside & mid[i];
+        maxT[i] = (!mid[i] & (d[i] != 0.f)) ? (cand[i] - o[i]) * inv[i] : -1.f;
     }
-    int wp = maxT[0] < maxT[1] ? 1 : 0;
-    const float t01 = wp ? maxT[1] : maxT[0];
-    wp = t01 < maxT[2] ? 2 : wp;
-    const float tw = wp == 2 ? maxT[2] : t01;
+    const bool w1 = maxT[0] < maxT[1];
+    const float t01 = w1 ? maxT[1] : maxT[0];
+    const bool w2 = t01 < maxT[2];
+    const float tw = w2 ? maxT[2] : t01;
+    const bool on[3] = {(bool)(!w1 & !w2), (bool)(w1 & !w2), w2};
     bool out = tw < 0.f;
     float coord[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float c = o[i] + tw * d[i];
-        const bool on = wp == i;
-        coord[i] = on ? cand[i] : c;
-        out = out || (!on && (c < mn[i] || c > mx[i]));
+        coord[i] = on[i] ? cand[i] : c;
+        out = out | (!on[i] & ((c < mn[i]) | (c > mx[i])));
     }
     if (DIST) {
         const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
@@ -156,7 +140,7 @@ __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], co
 __device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriHit &h) {
     const V3 p = rtv::cross(r.d, V);
     const float det = rtv::dot(U, p);
-    const bool ok_det = !(-1e-6 < (double)det && (double)det < 1e-6);
+    const bool ok_det = !((-1e-6 < (double)det) & ((double)det < 1e-6));
     const float inv_det = 1.f / det;
     const V3 s = rtv::sub(r.o, v0);
     const float u = inv_det * rtv::dot(s, p);
@@ -166,7 +150,46 @@ __device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriH
     h.t = t;
     h.u = u;
     h.v = v;
-    return ok_det && !(u < 0 || u > 1) && !(v < 0 || u + v > 1) && !(t < 0.f);
+    return ok_det & !((u < 0) | (u > 1)) & !((v < 0) | (u + v > 1)) & !(t < 0.f);
+}
+
+// Queues hold the rays themselves, 48 bytes per entry, so the extend kernel gets a ray with
+// three coalesced 16-byte loads and nothing to recompute:
+//   [3q]     (origin, slot bits)
+//   [3q + 1] (dir, bits: dir-sign mask (bit i: dir[i] > 0) | root-box miss << 3)
+//   [3q + 2] (1 / dir, 0)             -- Ray::Ray's inv_direction, computed once by the producer
+// The producer (wf_init / wf_shade) also runs the root box test of BVH::intersect
+// (bvh.cpp:239-243), a pure function of the ray, so traversal lanes start at the root's
+// children.  Hits are written by queue position, 16 bytes: (t, u, v, prim bits).
+constexpr int kQRec = 3;   // float4 per queue entry
+__device__ __forceinline__ void store_qray(const DevScene &sc, float4 *q, unsigned p, int slot, const Ray &r) {
+    const NodeRec root = load_node(sc.node, 0);
+    float e;
+    const bool hit = box_hit<false>(root.mn, root.mx, r, e);
+    const uint32_t bits = (r.d.x > 0 ? 1u : 0u) | (r.d.y > 0 ? 2u : 0u) | (r.d.z > 0 ? 4u : 0u) | (hit ? 0u : 8u);
+    q[kQRec * (size_t)p] = make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(slot));
+    q[kQRec * (size_t)p + 1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(bits));
+    q[kQRec * (size_t)p + 2] = make_float4(r.inv.x, r.inv.y, r.inv.z, 0.f);
+}
+// The ray as the shade kernel needs it (origin, direction).
+__device__ __forceinline__ Ray load_qray(const float4 *q, unsigned p, int &slot) {
+    const float4 a = q[kQRec * (size_t)p], b = q[kQRec * (size_t)p + 1];
+    Ray r;
+    r.o = V3{a.x, a.y, a.z};
+    r.d = V3{b.x, b.y, b.z};
+    r.inv = V3{0.f, 0.f, 0.f};
+    slot = __float_as_int(a.w);
+    return r;
+}
+// The ray as the extend kernel needs it (+ inv_direction, dir signs, root-box result).
+__device__ __forceinline__ Ray load_qray_trav(const float4 *q, unsigned p, uint32_t &bits) {
+    const float4 a = q[kQRec * (size_t)p], b = q[kQRec * (size_t)p + 1], c = q[kQRec * (size_t)p + 2];
+    Ray r;
+    r.o = V3{a.x, a.y, a.z};
+    r.d = V3{b.x, b.y, b.z};
+    r.inv = V3{c.x, c.y, c.z};
+    bits = __float_as_uint(b.w);
+    return r;
 }
 
 // Resumable traversal state of one ray.
@@ -177,6 +200,7 @@ struct TravState {
     float acc;       // best t inside the subtree being traversed (the reference's local best)
     int sp;
     int phase;
+    uint32_t dpos;   // bit i: dir[i] > 0 (near-child choice, bvh.cpp:196-203)
     Hit best;        // global winner so far (strict <, first of equal t wins)
 };
 
@@ -197,20 +221,21 @@ __device__ __forceinline__ void trav_enter(TravState &T, uint32_t a, uint32_t b)
     T.phase = b < 3u ? TP_NODE : (T.kend > T.k ? TP_LEAF : TP_POP);
 }
 
-// BVH::intersect entry (bvh.cpp:239-243): counters, root box.  False = the ray misses the
-// scene (T.best says so).
+// BVH::intersect entry (bvh.cpp:239-243) for a queued ray: counters, and the root box
+// result the producer stored (bits from load_qray_trav).  False = the ray misses the scene
+// (T.best says so).  (root_a, root_b) are the root node's fields.
 template <bool COUNT>
-__device__ __forceinline__ bool trav_start(const DevScene &sc, const Ray &r, TravState &T, Counters &cnt) {
+__device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint32_t root_b, TravState &T,
+                                           Counters &cnt) {
     if (COUNT) { cnt.rays++; cnt.aabb++; }
     T.best.t = 1e9f;
     T.best.prim = -1;
     T.best.u = T.best.v = 0.f;
     T.sp = 0;
     T.acc = 1e9f;
-    const NodeRec root = load_node(sc.node, 0);
-    trav_enter(T, root.a, root.b);
-    float e;
-    return box_hit<false>(root.mn, root.mx, r, e);
+    T.dpos = bits & 7u;
+    trav_enter(T, root_a, root_b);
+    return (bits & 8u) == 0;
 }
 
 // One unit of traversal work: the child pair of one internal node, or one leaf triangle,
@@ -225,8 +250,7 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
         NodeRec L, R;
         load_pair(sc.node, a, L, R);
         if (COUNT) cnt.aabb += 2;
-        const float ds = b == 0 ? r.d.x : (b == 1 ? r.d.y : r.d.z);
-        const bool lf = ds > 0;
+        const bool lf = (T.dpos >> b) & 1u;   // dir[split axis] > 0: left child first
         NodeRec N, F;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -322,12 +346,17 @@ struct LdsStack {
 };
 #endif
 
-// The whole closest-hit query (host tests; the device kernel interleaves the steps of many rays).
+// The whole closest-hit query through a queue record (host tests; the device kernel
+// interleaves the steps of many rays).
 template <bool COUNT>
-__device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const Ray &r, Hit &best, uint2 *stk, Counters &cnt) {
+__device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const float4 *q, unsigned p, Hit &best, uint2 *stk,
+                                               Counters &cnt) {
+    uint32_t bits;
+    const Ray r = load_qray_trav(q, p, bits);
+    const NodeRec root = load_node(sc.node, 0);
     TravState T;
     ArrayStack S{stk};
-    if (trav_start<COUNT>(sc, r, T, cnt))
+    if (trav_start<COUNT>(bits, root.a, root.b, T, cnt))
         while (!trav_step<COUNT>(sc, r, T, S, cnt)) {
         }
     best = T.best;

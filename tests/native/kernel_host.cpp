@@ -153,19 +153,17 @@ extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world
     st.rec = f.data() + 5 * n;
     st.rng_x = u.data();
     st.meta = u.data() + n;
-    std::vector<float4> q((size_t)2 * n), q2((size_t)2 * n), hits((size_t)n);
+    std::vector<float4> q((size_t)rtd::kQRec * n), q2((size_t)rtd::kQRec * n), hits((size_t)n);
     unsigned cnt_q = 0;
-    for (long long i = 0; i < n; ++i) rtd::store_qray(q.data(), cnt_q++, (int)i, rtd::wf_init_slot(sc, g, st, i));
+    for (long long i = 0; i < n; ++i) rtd::store_qray(sc, q.data(), cnt_q++, (int)i, rtd::wf_init_slot(sc, g, st, i));
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 stk[rtd::kStack];
     int64_t it = 0;
     while (cnt_q > 0) {
         if (++it > (int64_t)spp * D + 16) return -1;
         for (unsigned p = 0; p < cnt_q; ++p) {   // extend
-            int slot;
-            const rtd::Ray r = rtd::load_qray(q.data(), p, slot);
             rtd::Hit h;
-            rtd::closest_hit_wf<true>(sc, r, h, stk, cnt);
+            rtd::closest_hit_wf<true>(sc, q.data(), p, h, stk, cnt);
             rtd::store_hit(hits.data(), p, h);
         }
         unsigned cnt_q2 = 0;
@@ -173,7 +171,7 @@ extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world
             int slot;
             rtd::Ray r = rtd::load_qray(q.data(), p, slot);
             const rtd::Hit h = rtd::load_hit(hits.data(), p);
-            if (rtd::wf_shade_slot<true>(sc, g, st, spp, slot, r, h, out, cnt)) rtd::store_qray(q2.data(), cnt_q2++, slot, r);
+            if (rtd::wf_shade_slot<true>(sc, g, st, spp, slot, r, h, out, cnt)) rtd::store_qray(sc, q2.data(), cnt_q2++, slot, r);
         }
         q.swap(q2);
         cnt_q = cnt_q2;
