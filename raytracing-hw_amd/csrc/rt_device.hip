@@ -23,6 +23,7 @@
 using rtd::Counters;
 using rtd::DevScene;
 
+constexpr int kMaxGroups = 8;
 struct rt_device_scene {
     int device = -1;
     void *buf = nullptr;         // one allocation holding every array
@@ -37,8 +38,11 @@ struct rt_device_scene {
     rtd::WfState wf{};
     float4 *wf_queue[2] = {nullptr, nullptr};
     float4 *wf_hits = nullptr;
-    unsigned *wf_count = nullptr;  // [2]
-    unsigned *wf_host_count = nullptr;  // pinned
+    unsigned *wf_count = nullptr;       // per slot group: [4k] [4k+1] queue counts, [4k+2] extend ray counter
+    unsigned *wf_host_count = nullptr;  // pinned, per group
+    int wf_groups = 1;                  // slot groups, each on its own stream (RT_WF_GROUPS)
+    hipStream_t wf_stream[kMaxGroups] = {};
+    hipEvent_t wf_event[kMaxGroups + 1] = {};
     // tuning (RT_WF_REFILL, RT_WF_CHUNK, RT_WF_EXTEND_BLOCKS_PER_CU environment overrides, read at upload)
     int wf_refill = 8;
     int wf_chunk = 64;
@@ -157,11 +161,11 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
 
 // ------------------------------------------------------------------------ wavefront
 // (rt_wavefront.h) init -> { extend ; shade } until every slot has finished its samples.
-__global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, rtd::WfState st, float4 *qout,
-                                                       unsigned *cout) {
-    for (long long base = (long long)blockIdx.x * blockDim.x; base < st.n; base += (long long)gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, rtd::WfState st, long long i0,
+                                                       long long i1, float4 *qout, unsigned *cout) {
+    for (long long base = i0 + (long long)blockIdx.x * blockDim.x; base < i1; base += (long long)gridDim.x * blockDim.x) {
         const long long i = base + threadIdx.x;
-        const bool valid = i < st.n;
+        const bool valid = i < i1;
         rtd::Ray r;
         if (valid) r = rtd::wf_init_slot(sc, g, st, i);
         const unsigned p = rtd::queue_slot(valid, cout);
@@ -336,6 +340,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     d->cu_count = prop.multiProcessorCount;
     if (const char *e = std::getenv("RT_WF_REFILL")) d->wf_refill = std::max(1, std::min(64, std::atoi(e)));
     if (const char *e = std::getenv("RT_WF_CHUNK")) d->wf_chunk = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
     if (const char *e = std::getenv("RT_WF_EXTEND_BLOCKS_PER_CU")) d->wf_ext_bpc = std::max(0, std::atoi(e));
     uint8_t *b = (uint8_t *)d->buf;
     DevScene &ds = d->ds;
@@ -379,8 +384,12 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
                        + 2 * 4 * rtd::kQRec + 4;   // two ray queues (48 B / entry), hits (16 B / entry)
     const size_t bytes = (size_t)cap * 4 * (size_t)planes;
     HIP_TRY(hipMalloc(&d->wf_buf, bytes));
-    HIP_TRY(hipMalloc((void **)&d->wf_count, 64));
-    HIP_TRY(hipHostMalloc((void **)&d->wf_host_count, 64, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void **)&d->wf_count, 16 * kMaxGroups));
+    HIP_TRY(hipHostMalloc((void **)&d->wf_host_count, 16 * kMaxGroups, hipHostMallocDefault));
+    for (int k = 0; k < d->wf_groups; ++k)
+        if (!d->wf_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&d->wf_stream[k], hipStreamNonBlocking));
+    for (int k = 0; k <= d->wf_groups; ++k)
+        if (!d->wf_event[k]) HIP_TRY(hipEventCreateWithFlags(&d->wf_event[k], hipEventDisableTiming));
     float *f = (float *)d->wf_buf;
     auto take = [&](int k) { float *p = f; f += (size_t)cap * k; return p; };
     rtd::WfState &w = d->wf;
@@ -443,6 +452,9 @@ struct LaunchTimer {
     }
 };
 
+// The slots are split into wf_groups contiguous groups, each iterating { extend ; shade }
+// on its own stream with its own queues, so one group's kernels fill the CUs that another
+// group's draining launch leaves idle.  Groups never share a slot: results are unchanged.
 int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth, float *d_out, hipStream_t stream,
                      bool count, LaunchTimer &timer) {
     if (depth < 1 || depth > 15) return rt_fail(RT_ERR_LIMIT, "wavefront path: ray_depth must be in [1, 15]");
@@ -451,33 +463,69 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     if (rc) return rc;
     rtd::WfState w = d->wf;
     w.n = g.n_pixels;
-    HIP_TRY(hipMemsetAsync(d->wf_count, 0, 16, stream));   // counts [0], [1]; extend ray counter [2]
-    const unsigned init_blocks = (unsigned)std::min<long long>((g.n_pixels + 255) / 256, (long long)d->cu_count * 8);
-    hipLaunchKernelGGL(wf_init_kernel, dim3(init_blocks), dim3(256), 0, stream, d->ds, g, w, d->wf_queue[0], &d->wf_count[0]);
+    const int G = (int)std::min<long long>(d->wf_groups, std::max<long long>(1, g.n_pixels / 4096));
+    HIP_TRY(hipMemsetAsync(d->wf_count, 0, 16 * kMaxGroups, stream));
+    HIP_TRY(hipEventRecord(d->wf_event[G], stream));
+    long long lo[kMaxGroups], hi[kMaxGroups];
+    bool live[kMaxGroups];
+    for (int k = 0; k < G; ++k) {
+        lo[k] = g.n_pixels * k / G;
+        hi[k] = g.n_pixels * (k + 1) / G;
+        live[k] = hi[k] > lo[k];
+        HIP_TRY(hipStreamWaitEvent(d->wf_stream[k], d->wf_event[G], 0));
+    }
+    const long long per = (g.n_pixels + G - 1) / G;
+    const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, per, d->wf_ext_bpc)
+                                      : persistent_blocks(d, wf_extend_kernel<false>, per, d->wf_ext_bpc);
+    const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true>, per)
+                                     : persistent_blocks(d, wf_shade_kernel<false>, per);
+    for (int k = 0; k < G; ++k) {
+        if (!live[k]) continue;
+        const unsigned init_blocks = (unsigned)std::min<long long>((hi[k] - lo[k] + 255) / 256, (long long)d->cu_count * 8);
+        hipLaunchKernelGGL(wf_init_kernel, dim3(init_blocks), dim3(256), 0, d->wf_stream[k], d->ds, g, w, lo[k], hi[k],
+                           d->wf_queue[0] + rtd::kQRec * lo[k], &d->wf_count[4 * k]);
+    }
     HIP_TRY(hipGetLastError());
-    const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, g.n_pixels, d->wf_ext_bpc)
-                                      : persistent_blocks(d, wf_extend_kernel<false>, g.n_pixels, d->wf_ext_bpc);
-    const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true>, g.n_pixels)
-                                     : persistent_blocks(d, wf_shade_kernel<false>, g.n_pixels);
     const long long max_iter = (long long)spp * depth + 16;
     int cur = 0;
     for (long long it = 0;; ++it) {
         if (it > max_iter) return rt_fail(RT_ERR_DEVICE, "wavefront path did not drain (internal error)");
-        HIP_TRY(timer.mark(0, stream));
-        if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, &d->wf_count[2], &d->wf_count[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
-        else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, stream, d->ds, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, &d->wf_count[2], &d->wf_count[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
-        HIP_TRY(timer.mark(0, stream));
-        HIP_TRY(timer.mark(1, stream));
-        if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
-        else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, stream, d->ds, g, w, spp, d->wf_queue[cur], &d->wf_count[cur], d->wf_hits, d->wf_queue[1 - cur], &d->wf_count[1 - cur], &d->wf_count[2], d_out, d->counters);
-        HIP_TRY(timer.mark(1, stream));
+        for (int k = 0; k < G; ++k) {
+            if (!live[k]) continue;
+            hipStream_t sk = d->wf_stream[k];
+            float4 *qi = d->wf_queue[cur] + rtd::kQRec * lo[k], *qo = d->wf_queue[1 - cur] + rtd::kQRec * lo[k];
+            float4 *hits = d->wf_hits + lo[k];
+            unsigned *c = &d->wf_count[4 * k];
+            HIP_TRY(timer.mark(0, sk));
+            if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
+            else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
+            HIP_TRY(timer.mark(0, sk));
+            HIP_TRY(timer.mark(1, sk));
+            if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], hits, qo, &c[1 - cur], &c[2], d_out, d->counters);
+            else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], hits, qo, &c[1 - cur], &c[2], d_out, d->counters);
+            HIP_TRY(timer.mark(1, sk));
+        }
         HIP_TRY(hipGetLastError());
         cur = 1 - cur;
         if ((it & 7) == 7) {
-            HIP_TRY(hipMemcpyAsync(d->wf_host_count, &d->wf_count[cur], 4, hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));
-            if (*d->wf_host_count == 0) break;
+            for (int k = 0; k < G; ++k)
+                if (live[k])
+                    HIP_TRY(hipMemcpyAsync(&d->wf_host_count[k], &d->wf_count[4 * k + cur], 4, hipMemcpyDeviceToHost,
+                                           d->wf_stream[k]));
+            bool any = false;
+            for (int k = 0; k < G; ++k) {
+                if (!live[k]) continue;
+                HIP_TRY(hipStreamSynchronize(d->wf_stream[k]));
+                if (d->wf_host_count[k] == 0) live[k] = false;
+                any = any || live[k];
+            }
+            if (!any) break;
         }
+    }
+    // the caller's stream continues after every group
+    for (int k = 0; k < G; ++k) {
+        HIP_TRY(hipEventRecord(d->wf_event[k], d->wf_stream[k]));
+        HIP_TRY(hipStreamWaitEvent(stream, d->wf_event[k], 0));
     }
     return RT_OK;
 }
@@ -575,6 +623,10 @@ void rt_device_scene_release(rt_scene *s) {
         if (d->wf_buf) (void)hipFree(d->wf_buf);
         if (d->wf_count) (void)hipFree(d->wf_count);
         if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
+        for (hipStream_t &x : d->wf_stream)
+            if (x) (void)hipStreamDestroy(x);
+        for (hipEvent_t &x : d->wf_event)
+            if (x) (void)hipEventDestroy(x);
     }
     delete d;
     s->dev = nullptr;
