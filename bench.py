@@ -57,17 +57,28 @@ def load_scenes_module():
 
 
 def cpu_baseline(scene_path, width, height, spp, rows, threads):
-    """Time the reference's CPU path on a bounded sample (first `rows` rows, `spp` spp)."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close")
+    """Time the reference's CPU path on a bounded sample (first `rows` rows, `spp` spp).
+
+    The reference (oracle/_ref, built from /root/reference's sources by oracle/Makefile):
+    ref_render runs the sample loop of Scene::render (scene.cpp:31-44) and is timed;
+    ref_harness (same sources, counting wraps) counts the rays of the same sample."""
+    ref_dir = os.path.join(ROOT, "oracle", "_ref")
+    timer, counter = os.path.join(ref_dir, "ref_render"), os.path.join(ref_dir, "ref_harness")
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     sample = f"{width}x{rows} rows of the {width}x{height} frame at {spp} spp"
-    if os.path.exists(ref):
+    args = ["time", scene_path, str(width), str(height), str(spp), str(rows)]
+    if os.path.exists(timer) and os.path.exists(counter):
         try:
-            out = subprocess.run([ref, "time", scene_path, str(width), str(height), str(spp), str(rows)],
-                                 env=env, capture_output=True, text=True, timeout=600, check=True).stdout
-            r = json.loads(out.strip().splitlines()[-1])
-            return {"value": r["rays"] / r["seconds"] / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "reference",
-                    "sample": sample + " (reference Scene::render loop, counting build)", "seconds": r["seconds"]}
+            def run(exe):
+                out = subprocess.run([exe, *args], env=env, capture_output=True, text=True, timeout=600,
+                                     check=True).stdout
+                return json.loads(out.strip().splitlines()[-1])
+            t = run(timer)
+            c = run(counter)
+            return {"value": c["rays"] / t["seconds"] / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                    "sample": sample + " (reference Scene::render sample loop; rays counted by a second, counting "
+                                       "build of the same sources)",
+                    "seconds": t["seconds"], "rays": c["rays"]}
         except Exception as e:  # noqa: BLE001
             print(f"[bench] reference CPU baseline failed: {e}", file=sys.stderr)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
