@@ -526,6 +526,23 @@ struct SoARec {
 // the path continues, its BRDF factors), advances nv and replaces r by the bounce ray.
 // Returns false where the recursion returns at this vertex (sample below the surface,
 // pdf <= 0 or NaN).
+// SceneDistribution::sample (random.cpp:194-208): mixture of cosine, VNDF and light
+// sampling chosen by one uniform(-1, 1) draw.
+__device__ __forceinline__ V3 scene_sample(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, Rng &rng) {
+    float s = (rng_uniform_m11(rng) + 1.f) * 3 * 0.5f;
+    if (!sc.n_lights) s /= 1.5f;
+    if (s <= 1.f) return cosine_sample(N, rng);
+    if (s <= 2.f) return vndf_sample(N, eye, r2, rng);
+    return light_sample(sc, pos, rng);
+}
+
+// SceneDistribution::pdf (random.cpp:210-218)
+template <bool COUNT>
+__device__ __forceinline__ float scene_pdf(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, V3 dir, Counters &cnt) {
+    if (!sc.n_lights) return (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
+    return (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt) + vndf_pdf(N, eye, r2, dir)) / 3;
+}
+
 template <bool COUNT, class Rec>
 __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
     if (COUNT) cnt.hits++;
@@ -575,24 +592,13 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     r2 = rtv::smax(kRoughness2Limit, r2);
     const V3 pos = rtv::add(r.o, rtv::mul(r.d, hit.t));
     const V3 eye = rtv::neg(r.d);
-    // SceneDistribution::sample (random.cpp:194-208)
-    V3 dir;
-    {
-        float s = (rng_uniform_m11(rng) + 1.f) * 3 * 0.5f;
-        if (!sc.n_lights) s /= 1.5f;
-        if (s <= 1.f) dir = cosine_sample(N, rng);
-        else if (s <= 2.f) dir = vndf_sample(N, eye, r2, rng);
-        else dir = light_sample(sc, pos, rng);
-    }
+    const V3 dir = scene_sample(sc, pos, N, eye, r2, rng);
     nv++;
     if (rtv::dot(dir, N) <= 0.f) {
         if (rtv::dot(dir, ngeo) <= 0.f) return false;
         N = ngeo;
     }
-    // SceneDistribution::pdf (random.cpp:210-218)
-    float pdf;
-    if (!sc.n_lights) pdf = (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
-    else pdf = (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt) + vndf_pdf(N, eye, r2, dir)) / 3;
+    const float pdf = scene_pdf<COUNT>(sc, pos, N, eye, r2, dir, cnt);
     if (pdf <= 0.f || isnan(pdf)) return false;
     // BRDF of this vertex (scene.cpp:134-154): used only if the child ray hits
     const float coeff = 1 / pdf;

@@ -181,3 +181,33 @@ extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world
     if (iterations) *iterations = it;
     return 0;
 }
+
+// SceneDistribution sample + pdf from explicit shading frames (the sampler goldens):
+// frame = (point, normal, eye, roughness2); each draw starts from Rng(seed) with an empty
+// normal cache; next_out = the engine's next output after the draw (pins draws consumed).
+extern "C" void kh_samplers(const rt_scene_view *v, int64_t n, const float *frame, const uint32_t *seed,
+                            float *dir_out, float *pdf_out, uint32_t *next_out) {
+    rtd::DevScene sc = make(v);
+    for (int64_t k = 0; k < n; ++k) {
+        const float *f = frame + 10 * k;
+        const rtv::V3 pos{f[0], f[1], f[2]}, N{f[3], f[4], f[5]}, eye{f[6], f[7], f[8]};
+        rtd::Rng rng{seed[k], 0u, 0.f};
+        rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
+        const rtv::V3 d = rtd::scene_sample(sc, pos, N, eye, f[9], rng);
+        pdf_out[k] = rtd::scene_pdf<false>(sc, pos, N, eye, f[9], d, cnt);
+        dir_out[3 * k] = d.x;
+        dir_out[3 * k + 1] = d.y;
+        dir_out[3 * k + 2] = d.z;
+        next_out[k] = rtd::rng_next(rng);
+    }
+}
+
+// Raw sequences: kind 0 = engine outputs, 1 = uniform(-1, 1), 2 = normal(0, 1).
+extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *out_u) {
+    rtd::Rng rng{seed, 0u, 0.f};
+    for (int k = 0; k < n; ++k) {
+        if (kind == 0) out_u[k] = rtd::rng_next(rng);
+        else if (kind == 1) out_f[k] = rtd::rng_uniform_m11(rng);
+        else out_f[k] = rtd::rng_normal(rng);
+    }
+}

@@ -101,3 +101,38 @@ def test_wave_kernel_emulation(rt, kh, waves):
     assert kh.kh_render_wave(ctypes.addressof(v), s, 0, 1, 8, waves, out.ctypes.data, cnt.ctypes.data) == 0
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert list(cnt[:6]) == list(cnt_want)
+
+
+def test_scene_sampler_matches_reference(rt, kh):
+    """SceneDistribution::sample / ::pdf (random.cpp:194-218) of the kernel source against the
+    reference on 2000 random shading frames, including the number of RNG draws consumed."""
+    g = rtref.golden("cornell_samplers.rtd")
+    v, keep = _view(rt, "cornell", 64, 64, 1)
+    n = len(g["seed"])
+    frame = np.ascontiguousarray(g["frame"], np.float32)
+    seed = np.ascontiguousarray(g["seed"], np.uint32)
+    d = np.zeros((n, 3), np.float32)
+    pdf = np.zeros(n, np.float32)
+    nxt = np.zeros(n, np.uint32)
+    kh.kh_samplers.argtypes = [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_void_p] * 5
+    kh.kh_samplers(ctypes.addressof(v), n, frame.ctypes.data, seed.ctypes.data, d.ctypes.data, pdf.ctypes.data,
+                   nxt.ctypes.data)
+    assert np.array_equal(rtref.bits(d), rtref.bits(g["dir"]))
+    assert np.array_equal(rtref.bits(pdf), rtref.bits(g["pdf"]))
+    assert np.array_equal(nxt, g["next"])
+
+
+def test_rng_sequences_match_reference(kh):
+    """minstd_rand0 engine, uniform_real_distribution(-1, 1) and the polar normal_distribution
+    (random.cpp:12-46, libstdc++ random.tcc) for five seeds."""
+    g = rtref.golden("cornell_samplers.rtd")
+    kh.kh_rng.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    for row, seed in enumerate([1, 2, 12345, 2147483646, 65536]):
+        u = np.zeros(8, np.uint32)
+        f = np.zeros(8, np.float32)
+        kh.kh_rng(seed, 0, 8, f.ctypes.data, u.ctypes.data)
+        assert np.array_equal(u, g["raw_engine"][row])
+        kh.kh_rng(seed, 1, 8, f.ctypes.data, u.ctypes.data)
+        assert np.array_equal(rtref.bits(f), rtref.bits(g["raw_uniform"][row]))
+        kh.kh_rng(seed, 2, 8, f.ctypes.data, u.ctypes.data)
+        assert np.array_equal(rtref.bits(f), rtref.bits(g["raw_normal"][row]))
