@@ -380,7 +380,7 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     d->wf_count = nullptr;
     d->wf_host_count = nullptr;
     const long long cap = ((n + 255) / 256) * 256;
-    const int planes = 2 + 1 + 3 + 9 * D      // rng, meta, sums, vertex records (per slot)
+    const int planes = 8 + 9 * D              // slot state (2 x 16 B), vertex records (36 B each)
                        + 2 * 4 * rtd::kQRec + 4;   // two ray queues (48 B / entry), hits (16 B / entry)
     const size_t bytes = (size_t)cap * 4 * (size_t)planes;
     HIP_TRY(hipMalloc(&d->wf_buf, bytes));
@@ -391,18 +391,16 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     for (int k = 0; k <= d->wf_groups; ++k)
         if (!d->wf_event[k]) HIP_TRY(hipEventCreateWithFlags(&d->wf_event[k], hipEventDisableTiming));
     float *f = (float *)d->wf_buf;
-    auto take = [&](int k) { float *p = f; f += (size_t)cap * k; return p; };
+    auto take = [&](long long k) { float *p = f; f += (size_t)cap * k; return p; };
     rtd::WfState &w = d->wf;
     w.n = n;
     w.D = D;
     d->wf_queue[0] = (float4 *)take(4 * rtd::kQRec);   // 16-B aligned: cap is a multiple of 256
     d->wf_queue[1] = (float4 *)take(4 * rtd::kQRec);
     d->wf_hits = (float4 *)take(4);
-    w.rng_x = (uint32_t *)take(1);
-    w.rng_saved = take(1);
-    w.meta = (uint32_t *)take(1);
-    w.sx = take(1); w.sy = take(1); w.sz = take(1);
-    w.rec = take(9 * D);
+    w.st = (float4 *)take(8);
+    w.rec_ab = (float4 *)take(8 * D);
+    w.rec_c = take(D);
     d->wf_cap = cap;
     d->wf_D = D;
     return RT_OK;

@@ -522,10 +522,6 @@ struct SoARec {
     __device__ __forceinline__ float get_alpha(int k) const { return at(8, k); }
 };
 
-// One hit of Scene::intersect (scene.cpp:85-154): records vertex nv (its emission and, if
-// the path continues, its BRDF factors), advances nv and replaces r by the bounce ray.
-// Returns false where the recursion returns at this vertex (sample below the surface,
-// pdf <= 0 or NaN).
 // SceneDistribution::sample (random.cpp:194-208): mixture of cosine, VNDF and light
 // sampling chosen by one uniform(-1, 1) draw.
 __device__ __forceinline__ V3 scene_sample(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, Rng &rng) {
@@ -543,6 +539,41 @@ __device__ __forceinline__ float scene_pdf(const DevScene &sc, V3 pos, V3 N, V3 
     return (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt) + vndf_pdf(N, eye, r2, dir)) / 3;
 }
 
+// The records of one path slot in HBM for the wavefront pipeline, vertex-major so a vertex
+// is two 16-byte stores and one 4-byte store: ab[2 * (i * D + k)] = (e.xyz, coeff),
+// ab[... + 1] = (m.xyz, cos), c[i * D + k] = alpha.  The emission is kept in registers until
+// the vertex's BRDF is known (set_brdf) or the path ends there (flush_e).
+struct AosRec {
+    float4 *ab;
+    float *c;
+    long long i;
+    int D;
+    V3 e;
+    int ek;
+    bool pending;
+    __device__ __forceinline__ long long v(int k) const { return i * D + k; }
+    __device__ __forceinline__ void set_e(int k, V3 x) { e = x; ek = k; pending = true; }
+    __device__ __forceinline__ void set_brdf(int k, V3 mm, float cf, float cs, float a) {
+        ab[2 * v(k)] = make_float4(e.x, e.y, e.z, cf);
+        ab[2 * v(k) + 1] = make_float4(mm.x, mm.y, mm.z, cs);
+        c[v(k)] = a;
+        pending = false;
+    }
+    __device__ __forceinline__ void flush_e() {
+        if (pending) ab[2 * v(ek)] = make_float4(e.x, e.y, e.z, 0.f);
+        pending = false;
+    }
+    __device__ __forceinline__ V3 get_e(int k) const { const float4 a = ab[2 * v(k)]; return V3{a.x, a.y, a.z}; }
+    __device__ __forceinline__ V3 get_m(int k) const { const float4 b = ab[2 * v(k) + 1]; return V3{b.x, b.y, b.z}; }
+    __device__ __forceinline__ float get_coeff(int k) const { return ab[2 * v(k)].w; }
+    __device__ __forceinline__ float get_cos(int k) const { return ab[2 * v(k) + 1].w; }
+    __device__ __forceinline__ float get_alpha(int k) const { return c[v(k)]; }
+};
+
+// One hit of Scene::intersect (scene.cpp:85-154): records vertex nv (its emission and, if
+// the path continues, its BRDF factors), advances nv and replaces r by the bounce ray.
+// Returns false where the recursion returns at this vertex (sample below the surface,
+// pdf <= 0 or NaN).
 template <bool COUNT, class Rec>
 __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
     if (COUNT) cnt.hits++;

@@ -21,12 +21,12 @@ namespace rtd {
 struct WfState {
     long long n;      // path slots (= pixels of the shard)
     int D;            // vertex records per slot (= ray_depth)
-    uint32_t *rng_x;
-    float *rng_saved;
-    uint32_t *meta;                       // s (bits 0-19), power (20-23), nv (24-27), saved flag (28)
-    float *sx, *sy, *sz;                  // pixel sums
-    float *rec;                           // 9 * D planes of n floats (SoARec)
+    float4 *st;       // 2 per slot: (rng state bits, normal cache, meta bits, 0), (pixel sum, 0)
+    float4 *rec_ab;   // AosRec: 2 per slot and vertex
+    float *rec_c;     //         1 per slot and vertex
 };
+// meta: samples done (bits 0-19), depth budget left (20-23), vertices recorded (24-27),
+// normal cache valid (28)
 
 __device__ __forceinline__ void store_hit(float4 *hits, unsigned p, const Hit &h) {
     hits[p] = make_float4(h.t, h.u, h.v, __int_as_float(h.prim));
@@ -384,10 +384,8 @@ __device__ __forceinline__ Ray wf_init_slot(const DevScene &sc, const ShardGeom 
     Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
     int power = 0;
     const Ray r = start_sample(sc, g, i, rng, power);
-    st.sx[i] = st.sy[i] = st.sz[i] = 0.f;
-    st.rng_x[i] = rng.x;
-    st.rng_saved[i] = rng.saved;
-    st.meta[i] = meta_pack(0, power, 0, rng.saved_avail);
+    st.st[2 * i] = make_float4(__uint_as_float(rng.x), rng.saved, __uint_as_float(meta_pack(0, power, 0, rng.saved_avail)), 0.f);
+    st.st[2 * i + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
     return r;
 }
 
@@ -398,22 +396,23 @@ __device__ __forceinline__ Ray wf_init_slot(const DevScene &sc, const ShardGeom 
 template <bool COUNT>
 __device__ __forceinline__ bool wf_shade_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, int spp,
                                               long long i, Ray &r, const Hit &h, float *out, Counters &cnt) {
-    const uint32_t meta = st.meta[i];
+    const float4 s0 = st.st[2 * i];
+    const uint32_t meta = __float_as_uint(s0.z);
     int s = (int)(meta & 0xfffffu), power = (int)((meta >> 20) & 15u), nv = (int)((meta >> 24) & 15u);
-    Rng rng{st.rng_x[i], (meta >> 28) & 1u, st.rng_saved[i]};
-    SoARec P{st.rec, st.n, i, st.D};
+    Rng rng{__float_as_uint(s0.x), (meta >> 28) & 1u, s0.y};
+    AosRec P{st.rec_ab, st.rec_c, i, st.D, V3{0.f, 0.f, 0.f}, 0, false};
     bool next = false;
     // the recursion continues with the bounce ray while calls remain (scene.cpp:72-75)
     if (h.prim >= 0 && h.t < sc.max_distance && shade_hit<COUNT>(sc, r, h, rng, cnt, P, nv) && power > 0) {
         power -= 1;
         next = true;
     }
+    P.flush_e();
     if (!next) {
         const V3 c = fold_path(P, nv);
-        const float ax = st.sx[i] + c.x, ay = st.sy[i] + c.y, az = st.sz[i] + c.z;
-        st.sx[i] = ax;
-        st.sy[i] = ay;
-        st.sz[i] = az;
+        const float4 s1 = st.st[2 * i + 1];
+        const float ax = s1.x + c.x, ay = s1.y + c.y, az = s1.z + c.z;
+        st.st[2 * i + 1] = make_float4(ax, ay, az, 0.f);
         if (++s == spp) {
             out[3 * i + 0] = ax;
             out[3 * i + 1] = ay;
@@ -424,9 +423,7 @@ __device__ __forceinline__ bool wf_shade_slot(const DevScene &sc, const ShardGeo
             next = true;
         }
     }
-    st.meta[i] = meta_pack(s, power, nv, rng.saved_avail);
-    st.rng_x[i] = rng.x;
-    st.rng_saved[i] = rng.saved;
+    st.st[2 * i] = make_float4(__uint_as_float(rng.x), rng.saved, __uint_as_float(meta_pack(s, power, nv, rng.saved_avail)), 0.f);
     return next;
 }
 

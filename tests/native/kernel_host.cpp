@@ -141,18 +141,14 @@ extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world
     const long long n = (long long)rows * v->width;
     rtd::ShardGeom g{v->width, rank, world, row_block, n};
     const int D = v->ray_depth;
-    std::vector<float> f((size_t)n * (5 + 9 * D));
-    std::vector<uint32_t> u((size_t)n * 2);
+    std::vector<float4> stv((size_t)2 * n), ab((size_t)2 * n * D);
+    std::vector<float> cv((size_t)n * D);
     rtd::WfState st{};
     st.n = n;
     st.D = D;
-    st.rng_saved = f.data();
-    st.sx = f.data() + n;
-    st.sy = f.data() + 2 * n;
-    st.sz = f.data() + 3 * n;
-    st.rec = f.data() + 5 * n;
-    st.rng_x = u.data();
-    st.meta = u.data() + n;
+    st.st = stv.data();
+    st.rec_ab = ab.data();
+    st.rec_c = cv.data();
     std::vector<float4> q((size_t)rtd::kQRec * n), q2((size_t)rtd::kQRec * n), hits((size_t)n);
     unsigned cnt_q = 0;
     for (long long i = 0; i < n; ++i) rtd::store_qray(sc, q.data(), cnt_q++, (int)i, rtd::wf_init_slot(sc, g, st, i));
