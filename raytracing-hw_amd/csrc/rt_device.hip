@@ -238,11 +238,36 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
     rtd::counters_flush<COUNT>(cnt, counters);
 }
 
-template <bool COUNT>
-__global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp,
+// Per-block LDS copies of the small tables every shading hit reads with a lane-dependent
+// index (texel decode LUT, materials): LDS reads instead of divergent vector-memory gathers.
+constexpr int kMatLds = 64;
+struct ShadeLds {
+    float lut[512];
+    float mf[kMatLds * 12];
+    int mt[kMatLds * 4];
+    double nt[kMatLds * 16];
+};
+
+template <bool COUNT, bool MAT_LDS>
+__global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp,
                                                         const float4 *qin, const unsigned *cin, const float4 *hits,
                                                         float4 *qout, unsigned *cout, unsigned *fetch, float *out,
                                                         unsigned long long *counters) {
+    __shared__ ShadeLds L;
+    for (int k = threadIdx.x; k < 512; k += blockDim.x) L.lut[k] = sc_in.lut[k];
+    if (MAT_LDS) {
+        for (int k = threadIdx.x; k < sc_in.n_meshes * 12; k += blockDim.x) L.mf[k] = sc_in.mesh_f[k];
+        for (int k = threadIdx.x; k < sc_in.n_meshes * 4; k += blockDim.x) L.mt[k] = sc_in.mesh_tex[k];
+        for (int k = threadIdx.x; k < sc_in.n_meshes * 16; k += blockDim.x) L.nt[k] = sc_in.mesh_nt[k];
+    }
+    __syncthreads();
+    DevScene sc = sc_in;
+    sc.lut = L.lut;
+    if (MAT_LDS) {
+        sc.mesh_f = L.mf;
+        sc.mesh_tex = L.mt;
+        sc.mesh_nt = L.nt;
+    }
     const unsigned n = *cin;
     if (blockIdx.x == 0 && threadIdx.x == 0) *fetch = 0;   // the next extend launch's ray counter
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -320,6 +345,9 @@ int ensure_device_scene(rt_scene *s, int device) {
                  o_lnode = append(blob, s->light_node), o_mf = append(blob, s->mesh_f),
                  o_mt = append(blob, s->mesh_tex), o_nt = append(blob, s->mesh_nt), o_ti = append(blob, s->tex_info),
                  o_tx = append(blob, s->texels);
+    std::vector<float> lut(512);
+    rtd::fill_decode_lut(lut.data());
+    const size_t o_lut = append(blob, lut);
     // node array at +32 B: sibling pairs (left odd, left + 1) share one 64-B line
     blob.resize(((blob.size() + 255) & ~size_t(255)) + 256);
     rt_device_scene *d = new rt_device_scene();
@@ -355,6 +383,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.mesh_nt = (const double *)(b + o_nt);
     ds.tex_info = (const uint4 *)(b + o_ti);
     ds.texels = (const uint32_t *)(b + o_tx);
+    ds.lut = (const float *)(b + o_lut);
     ds.n_lights = (int)(s->light.size() / 16);
     ds.n_tris = (int)(s->tri.size() / 12);
     ds.n_nodes = (int)(s->node.size() / 8);
@@ -475,8 +504,9 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     const long long per = (g.n_pixels + G - 1) / G;
     const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, per, d->wf_ext_bpc)
                                       : persistent_blocks(d, wf_extend_kernel<false>, per, d->wf_ext_bpc);
-    const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true>, per)
-                                     : persistent_blocks(d, wf_shade_kernel<false>, per);
+    const bool mat_lds = d->ds.n_meshes <= kMatLds;
+    const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true, true>, per)
+                                     : persistent_blocks(d, wf_shade_kernel<false, true>, per);
     for (int k = 0; k < G; ++k) {
         if (!live[k]) continue;
         const unsigned init_blocks = (unsigned)std::min<long long>((hi[k] - lo[k] + 255) / 256, (long long)d->cu_count * 8);
@@ -499,8 +529,9 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
             else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
             HIP_TRY(timer.mark(0, sk));
             HIP_TRY(timer.mark(1, sk));
-            if (count) hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], hits, qo, &c[1 - cur], &c[2], d_out, d->counters);
-            else hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], hits, qo, &c[1 - cur], &c[2], d_out, d->counters);
+            auto shade = count ? (mat_lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
+                               : (mat_lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
+            hipLaunchKernelGGL(shade, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], hits, qo, &c[1 - cur], &c[2], d_out, d->counters);
             HIP_TRY(timer.mark(1, sk));
         }
         HIP_TRY(hipGetLastError());

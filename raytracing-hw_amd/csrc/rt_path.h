@@ -59,6 +59,16 @@ constexpr float kInvPiF = 0.318309886183790671538f; // M_1_PIf32
 constexpr float kStep = 1e-4f;                      // scene.cpp:11 `const float step = 1e-4`
 constexpr float kRoughness2Limit = 0.03f;           // scene.cpp:15
 
+// Decode table for RGBA8 texels: 256 sRGB entries (rt_srgb_lut.h, glibc powf) then 256 linear
+// entries (float)(int)b / 255.f, the two decodes of Texture::interpolate_sample
+// (primitive.h:172-215).  Lives in the scene blob; kernels may stage it in LDS.
+inline void fill_decode_lut(float *lut) {
+    for (int b = 0; b < 256; ++b) {
+        lut[b] = rtm::kSrgbLut[b];
+        lut[256 + b] = (float)b / 255.f;
+    }
+}
+
 struct DevScene {
     const float4 *tri;        // 3 x float4 / triangle: (v0, U.x) (U.yz, V.xy) (V.z, n_geo)
     const float4 *tri_attr;   // 4 x float4 / triangle: normals, texcoords, mesh id
@@ -71,6 +81,7 @@ struct DevScene {
     const double *mesh_nt;    // 16 / mesh
     const uint4 *tex_info;    // texel offset, width, height, channels
     const uint32_t *texels;   // RGBA8
+    const float *lut;         // 512: [b] = sRGB decode powf(b / 255.f, 2.2f), [256 + b] = b / 255.f
     int n_lights;
     int n_tris, n_nodes, n_meshes;
     int ray_depth;
@@ -380,7 +391,7 @@ __device__ __forceinline__ V4 tex_sample(const DevScene &sc, int tex, V2 p, bool
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t byte = (texel[k] >> (8 * c)) & 0xffu;
-            v[k] = srgb ? rtm::kSrgbLut[byte] : (float)(int)byte / 255.f;
+            v[k] = sc.lut[(srgb ? 0u : 256u) + byte];   // kSrgbLut[byte] or (float)(int)byte / 255.f
         }
         res[c] = v[0] * (1 - dx) * (1 - dy) + v[1] * (1 - dx) * dy + v[2] * dx * (1 - dy) + v[3] * dx * dy;
     }

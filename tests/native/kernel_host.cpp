@@ -20,6 +20,10 @@ static rtd::DevScene make(const rt_scene_view *v) {
     s.mesh_nt = v->mesh_normal_transform;
     s.tex_info = (const uint4 *)v->tex_info;
     s.texels = (const uint32_t *)v->texels;
+    static float lut[512];
+    static bool lut_ready = false;
+    if (!lut_ready) { rtd::fill_decode_lut(lut); lut_ready = true; }
+    s.lut = lut;
     s.n_lights = (int)v->n_lights;
     s.ray_depth = v->ray_depth;
     s.max_distance = v->max_distance;
