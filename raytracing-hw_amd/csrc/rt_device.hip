@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 #include <cstdlib>
+#include <type_traits>
 
 #include "rt_path.h"
 #include "rt_wave.h"
@@ -46,6 +47,8 @@ struct rt_device_scene {
     // tuning (RT_WF_REFILL, RT_WF_CHUNK, RT_WF_EXTEND_BLOCKS_PER_CU environment overrides, read at upload)
     int wf_refill = 8;
     int wf_chunk = 64;
+    int wf_node_lds = 0;  // top BVH levels in LDS (RT_WF_NODE_LDS)
+    double wf_compact_below = 0.5;  // dense queue until this fraction of slots is active (RT_WF_COMPACT_BELOW)
     int wf_ext_bpc = 0;   // 0 = as many as fit
 };
 
@@ -161,15 +164,19 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
 
 // ------------------------------------------------------------------------ wavefront
 // (rt_wavefront.h) init -> { extend ; shade } until every slot has finished its samples.
+// Queue modes.  Dense: entry p holds slot (slot0 + p)'s ray, or an inactive marker (slot
+// -1) once that pixel has all its samples; the order never changes, so a wave's lanes keep
+// neighbouring pixels (coherent camera rays, coalesced slot-state access) for the whole
+// frame.  Compact: active rays only, appended with one atomic per wave; used for the tail
+// of the frame, when most slots are finished.  In both modes *count is the number of
+// active rays (the host's termination test).
 __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, rtd::WfState st, long long i0,
                                                        long long i1, float4 *qout, unsigned *cout) {
     for (long long base = i0 + (long long)blockIdx.x * blockDim.x; base < i1; base += (long long)gridDim.x * blockDim.x) {
         const long long i = base + threadIdx.x;
         const bool valid = i < i1;
-        rtd::Ray r;
-        if (valid) r = rtd::wf_init_slot(sc, g, st, i);
-        const unsigned p = rtd::queue_slot(valid, cout);
-        if (valid) rtd::store_qray(sc, qout, p, (int)i, r);
+        if (valid) rtd::store_qray(sc, qout, (unsigned)(i - i0), (int)i, rtd::wf_init_slot(sc, g, st, i));
+        rtd::queue_slot(valid, cout);   // active count
     }
 }
 
@@ -180,11 +187,12 @@ __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, 
 // queue; a wave claims a new chunk of `chunk` entries with one atomic when its chunk runs
 // out (a single shared counter hit by every refill serialises all waves on one address).
 // The rays sit in the queue entries: one coalesced load each.
-template <bool COUNT>
+template <bool COUNT, bool NODE_LDS>
 __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float4 *qin, const unsigned *count,
-                                                         float4 *hits, unsigned *fetch, unsigned *next_count,
-                                                         unsigned long long *counters, int refill, unsigned chunk) {
-    const unsigned n = *count;
+                                                         unsigned npos, float4 *hits, unsigned *fetch,
+                                                         unsigned *next_count, unsigned long long *counters, int refill,
+                                                         unsigned chunk) {
+    const unsigned n = npos ? npos : *count;   // queue positions (dense: all slots of the group)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
         *next_count = 0;                                 // the shade kernel's output queue
@@ -193,6 +201,9 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
     uint2 spill[rtd::kStack - rtd::kLdsStack];
     rtd::LdsStack S{spill};
     const int lane = threadIdx.x & 63;
+    using Nodes = typename std::conditional<NODE_LDS, rtd::LdsNodes, rtd::GlobalNodes>::type;
+    if (NODE_LDS) rtd::LdsNodes::fill(sc.node, sc.n_nodes);
+    const Nodes nodes{sc.node};
     const rtd::NodeRec root = rtd::load_node(sc.node, 0);
     unsigned q = 0, lo = 0, hi = 0;   // [lo, hi): the wave's unclaimed part of its chunk
     bool busy = false, exhausted = false;
@@ -224,12 +235,15 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
             if (mine != 0xffffffffu) {
                 q = mine;
                 uint32_t bits;
-                r = rtd::load_qray_trav(qin, q, bits);
-                busy = rtd::trav_start<COUNT>(bits, root.a, root.b, T, cnt);
-                if (!busy) rtd::store_hit(hits, q, T.best);   // misses the scene box
+                int slot;
+                r = rtd::load_qray_trav(qin, q, bits, slot);
+                if (slot >= 0) {   // (dense queue: inactive entries are skipped)
+                    busy = rtd::trav_start<COUNT>(bits, root.a, root.b, T, cnt);
+                    if (!busy) rtd::store_hit(hits, q, T.best);   // misses the scene box
+                }
             }
         }
-        if (busy && rtd::trav_step<COUNT>(sc, r, T, S, cnt)) {
+        if (busy && rtd::trav_step<COUNT>(sc, r, T, S, nodes, cnt)) {
             rtd::store_hit(hits, q, T.best);
             busy = false;
         }
@@ -250,8 +264,9 @@ struct ShadeLds {
 
 template <bool COUNT, bool MAT_LDS>
 __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp,
-                                                        const float4 *qin, const unsigned *cin, const float4 *hits,
-                                                        float4 *qout, unsigned *cout, unsigned *fetch, float *out,
+                                                        const float4 *qin, const unsigned *cin, unsigned npos,
+                                                        const float4 *hits, float4 *qout, unsigned *cout,
+                                                        long long slot0, int dense_out, unsigned *fetch, float *out,
                                                         unsigned long long *counters) {
     __shared__ ShadeLds L;
     for (int k = threadIdx.x; k < 512; k += blockDim.x) L.lut[k] = sc_in.lut[k];
@@ -268,22 +283,28 @@ __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc_in, ShardGeom
         sc.mesh_tex = L.mt;
         sc.mesh_nt = L.nt;
     }
-    const unsigned n = *cin;
+    const unsigned n = npos ? npos : *cin;   // input positions (dense: all slots of the group)
     if (blockIdx.x == 0 && threadIdx.x == 0) *fetch = 0;   // the next extend launch's ray counter
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     for (unsigned base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const unsigned q = base + threadIdx.x;
-        const bool valid = q < n;
-        int slot = 0;
+        int slot = -1;
         bool next = false;
         rtd::Ray r;
-        if (valid) {
+        if (q < n) {
             r = rtd::load_qray(qin, q, slot);
-            const rtd::Hit h = rtd::load_hit(hits, q);
-            next = rtd::wf_shade_slot<COUNT>(sc, g, st, spp, slot, r, h, out, cnt);
+            if (slot >= 0) {
+                const rtd::Hit h = rtd::load_hit(hits, q);
+                next = rtd::wf_shade_slot<COUNT>(sc, g, st, spp, slot, r, h, out, cnt);
+            }
         }
         const unsigned p = rtd::queue_slot(next, cout);
-        if (next) rtd::store_qray(sc, qout, p, slot, r);
+        if (dense_out) {   // (dense out implies dense in: entry q is slot slot0 + q)
+            if (next) rtd::store_qray(sc, qout, q, slot, r);
+            else if (q < n) rtd::store_qray_inactive(qout, q);
+        } else if (next) {
+            rtd::store_qray(sc, qout, p, slot, r);
+        }
     }
     rtd::counters_flush<COUNT>(cnt, counters);
 }
@@ -322,6 +343,46 @@ size_t append(std::vector<uint8_t> &blob, const std::vector<T> &v, size_t pre = 
     return off;
 }
 
+// The device copy of the scene BVH is renumbered breadth-first: a node's children stay an
+// adjacent pair (right = left + 1) and leaves keep their triangle ranges, so traversal
+// visits, counters and results are unchanged, while the top levels become a prefix of the
+// array that the extend kernel keeps in LDS (rt_wavefront.h NodeCache).
+std::vector<float> bfs_nodes(const std::vector<float> &node) {
+    const size_t n = node.size() / 8;
+    std::vector<float> out(node.size());
+    if (n == 0) return out;
+    std::vector<uint32_t> order;   // old ids in new order
+    order.reserve(n);
+    order.push_back(0);
+    std::vector<uint32_t> new_id(n, 0);
+    for (size_t h = 0; h < order.size(); ++h) {
+        const uint32_t u = order[h];
+        uint32_t b;
+        std::memcpy(&b, &node[8 * u + 7], 4);
+        if (b < 3u) {
+            uint32_t a;
+            std::memcpy(&a, &node[8 * u + 6], 4);
+            new_id[a] = (uint32_t)order.size();
+            order.push_back(a);
+            new_id[a + 1] = (uint32_t)order.size();
+            order.push_back(a + 1);
+        }
+    }
+    for (size_t k = 0; k < order.size(); ++k) {
+        const uint32_t u = order[k];
+        std::memcpy(&out[8 * k], &node[8 * u], 8 * sizeof(float));
+        uint32_t b;
+        std::memcpy(&b, &node[8 * u + 7], 4);
+        if (b < 3u) {
+            uint32_t a;
+            std::memcpy(&a, &node[8 * u + 6], 4);
+            const uint32_t na = new_id[a];
+            std::memcpy(&out[8 * k + 6], &na, 4);
+        }
+    }
+    return out;
+}
+
 int ensure_device_scene(rt_scene *s, int device) {
     if (s->dev && s->dev->device == device) return RT_OK;
     if (s->dev) rt_device_scene_release(s);
@@ -341,7 +402,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     HIP_TRY(hipSetDevice(device));
     std::vector<uint8_t> blob;
     const size_t o_tri = append(blob, s->tri), o_attr = append(blob, s->tri_attr), o_tan = append(blob, s->tri_tan),
-                 o_node = append(blob, s->node, 32), o_light = append(blob, s->light),
+                 o_node = append(blob, bfs_nodes(s->node), 32), o_light = append(blob, s->light),
                  o_lnode = append(blob, s->light_node), o_mf = append(blob, s->mesh_f),
                  o_mt = append(blob, s->mesh_tex), o_nt = append(blob, s->mesh_nt), o_ti = append(blob, s->tex_info),
                  o_tx = append(blob, s->texels);
@@ -368,6 +429,8 @@ int ensure_device_scene(rt_scene *s, int device) {
     d->cu_count = prop.multiProcessorCount;
     if (const char *e = std::getenv("RT_WF_REFILL")) d->wf_refill = std::max(1, std::min(64, std::atoi(e)));
     if (const char *e = std::getenv("RT_WF_CHUNK")) d->wf_chunk = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("RT_WF_NODE_LDS")) d->wf_node_lds = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_WF_COMPACT_BELOW")) d->wf_compact_below = std::atof(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
     if (const char *e = std::getenv("RT_WF_EXTEND_BLOCKS_PER_CU")) d->wf_ext_bpc = std::max(0, std::atoi(e));
     uint8_t *b = (uint8_t *)d->buf;
@@ -494,16 +557,19 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     HIP_TRY(hipMemsetAsync(d->wf_count, 0, 16 * kMaxGroups, stream));
     HIP_TRY(hipEventRecord(d->wf_event[G], stream));
     long long lo[kMaxGroups], hi[kMaxGroups];
-    bool live[kMaxGroups];
+    bool live[kMaxGroups], dense[kMaxGroups], to_compact[kMaxGroups];
     for (int k = 0; k < G; ++k) {
         lo[k] = g.n_pixels * k / G;
         hi[k] = g.n_pixels * (k + 1) / G;
         live[k] = hi[k] > lo[k];
+        dense[k] = true;   // see wf_init_kernel: dense queue until most slots are done
+        to_compact[k] = false;
         HIP_TRY(hipStreamWaitEvent(d->wf_stream[k], d->wf_event[G], 0));
     }
     const long long per = (g.n_pixels + G - 1) / G;
-    const unsigned ext_blocks = count ? persistent_blocks(d, wf_extend_kernel<true>, per, d->wf_ext_bpc)
-                                      : persistent_blocks(d, wf_extend_kernel<false>, per, d->wf_ext_bpc);
+    auto extend = count ? (d->wf_node_lds ? wf_extend_kernel<true, true> : wf_extend_kernel<true, false>)
+                        : (d->wf_node_lds ? wf_extend_kernel<false, true> : wf_extend_kernel<false, false>);
+    const unsigned ext_blocks = persistent_blocks(d, extend, per, d->wf_ext_bpc);
     const bool mat_lds = d->ds.n_meshes <= kMatLds;
     const unsigned sh_blocks = count ? persistent_blocks(d, wf_shade_kernel<true, true>, per)
                                      : persistent_blocks(d, wf_shade_kernel<false, true>, per);
@@ -525,13 +591,15 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
             float4 *hits = d->wf_hits + lo[k];
             unsigned *c = &d->wf_count[4 * k];
             HIP_TRY(timer.mark(0, sk));
-            if (count) hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
-            else hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
+            const unsigned npos = dense[k] ? (unsigned)(hi[k] - lo[k]) : 0u;
+            hipLaunchKernelGGL(extend, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], npos, hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
             HIP_TRY(timer.mark(0, sk));
             HIP_TRY(timer.mark(1, sk));
             auto shade = count ? (mat_lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
                                : (mat_lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
-            hipLaunchKernelGGL(shade, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], hits, qo, &c[1 - cur], &c[2], d_out, d->counters);
+            const int dense_out = dense[k] && !to_compact[k];
+            hipLaunchKernelGGL(shade, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], npos, hits, qo, &c[1 - cur], (long long)lo[k], dense_out, &c[2], d_out, d->counters);
+            if (to_compact[k]) dense[k] = false;
             HIP_TRY(timer.mark(1, sk));
         }
         HIP_TRY(hipGetLastError());
@@ -546,6 +614,8 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
                 if (!live[k]) continue;
                 HIP_TRY(hipStreamSynchronize(d->wf_stream[k]));
                 if (d->wf_host_count[k] == 0) live[k] = false;
+                if (dense[k] && (double)d->wf_host_count[k] < d->wf_compact_below * (double)(hi[k] - lo[k]))
+                    to_compact[k] = true;
                 any = any || live[k];
             }
             if (!any) break;

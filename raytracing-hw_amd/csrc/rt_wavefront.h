@@ -182,14 +182,19 @@ __device__ __forceinline__ Ray load_qray(const float4 *q, unsigned p, int &slot)
     return r;
 }
 // The ray as the extend kernel needs it (+ inv_direction, dir signs, root-box result).
-__device__ __forceinline__ Ray load_qray_trav(const float4 *q, unsigned p, uint32_t &bits) {
+__device__ __forceinline__ Ray load_qray_trav(const float4 *q, unsigned p, uint32_t &bits, int &slot) {
     const float4 a = q[kQRec * (size_t)p], b = q[kQRec * (size_t)p + 1], c = q[kQRec * (size_t)p + 2];
     Ray r;
     r.o = V3{a.x, a.y, a.z};
     r.d = V3{b.x, b.y, b.z};
     r.inv = V3{c.x, c.y, c.z};
     bits = __float_as_uint(b.w);
+    slot = __float_as_int(a.w);
     return r;
+}
+// Dense-queue entry of a slot that has finished all its samples.
+__device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
+    q[kQRec * (size_t)p] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
 }
 
 // Resumable traversal state of one ray.
@@ -202,6 +207,14 @@ struct TravState {
     int phase;
     uint32_t dpos;   // bit i: dir[i] > 0 (near-child choice, bvh.cpp:196-203)
     Hit best;        // global winner so far (strict <, first of equal t wins)
+};
+
+// Where trav_step reads child pairs from: the node array in HBM ...
+struct GlobalNodes {
+    const float4 *node;
+    __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
+        rtd::load_pair(node, left, L, R);
+    }
 };
 
 // Host / test stack: a plain array.
@@ -242,13 +255,14 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
 // followed (when the subtree is finished) by the return up the frames until a far child
 // is to be visited.  Returns true once the stack is empty (T.best is final).  A wave's
 // lanes each advance by one unit per call, whatever mix of units they are at.
-template <bool COUNT, class Stack>
-__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, Counters &cnt) {
+template <bool COUNT, class Stack, class Nodes>
+__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, const Nodes &nodes,
+                                          Counters &cnt) {
     if (T.phase == TP_NODE) {
         const uint32_t a = T.a, b = T.b;
         RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, T.a = 0);
         NodeRec L, R;
-        load_pair(sc.node, a, L, R);
+        nodes.load_pair(a, L, R);
         if (COUNT) cnt.aabb += 2;
         const bool lf = (T.dpos >> b) & 1u;   // dir[split axis] > 0: left child first
         NodeRec N, F;
@@ -344,6 +358,35 @@ struct LdsStack {
         return v;
     }
 };
+
+// ... or, for the top of the tree, LDS.  The device node array is breadth-first
+// (rt_device.hip bfs_nodes), so its first kLdsNodes nodes are the top levels, which nearly
+// every ray visits; each block keeps a copy and reads those pairs with ds_read.
+constexpr int kLdsNodes = 128;   // 4 KB: the top 7 levels of a full tree
+__shared__ float4 wf_lds_nodes[2 * kLdsNodes];
+struct LdsNodes {
+    const float4 *node;
+    __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
+        if (left + 1 < (uint32_t)kLdsNodes) {
+            const float4 p0 = wf_lds_nodes[2 * left], q0 = wf_lds_nodes[2 * left + 1];
+            const float4 p1 = wf_lds_nodes[2 * left + 2], q1 = wf_lds_nodes[2 * left + 3];
+            L.mn[0] = p0.x; L.mn[1] = p0.y; L.mn[2] = p0.z; L.mx[0] = p0.w; L.mx[1] = q0.x; L.mx[2] = q0.y;
+            L.a = __float_as_uint(q0.z); L.b = __float_as_uint(q0.w);
+            R.mn[0] = p1.x; R.mn[1] = p1.y; R.mn[2] = p1.z; R.mx[0] = p1.w; R.mx[1] = q1.x; R.mx[2] = q1.y;
+            R.a = __float_as_uint(q1.z); R.b = __float_as_uint(q1.w);
+        } else {
+            rtd::load_pair(node, left, L, R);
+            // keeps the two sources apart (merged, they become flat loads through a selected pointer)
+            asm volatile("" : "+v"(L.a), "+v"(R.a));
+        }
+    }
+    // block-cooperative fill; call before the first traversal, all threads of the block
+    __device__ __forceinline__ static void fill(const float4 *node, int n_nodes) {
+        const int m = 2 * (n_nodes < kLdsNodes ? n_nodes : kLdsNodes);
+        for (int k = threadIdx.x; k < m; k += blockDim.x) wf_lds_nodes[k] = node[k];
+        __syncthreads();
+    }
+};
 #endif
 
 // The whole closest-hit query through a queue record (host tests; the device kernel
@@ -352,12 +395,14 @@ template <bool COUNT>
 __device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const float4 *q, unsigned p, Hit &best, uint2 *stk,
                                                Counters &cnt) {
     uint32_t bits;
-    const Ray r = load_qray_trav(q, p, bits);
+    int slot;
+    const Ray r = load_qray_trav(q, p, bits, slot);
     const NodeRec root = load_node(sc.node, 0);
     TravState T;
     ArrayStack S{stk};
+    const GlobalNodes nodes{sc.node};
     if (trav_start<COUNT>(bits, root.a, root.b, T, cnt))
-        while (!trav_step<COUNT>(sc, r, T, S, cnt)) {
+        while (!trav_step<COUNT>(sc, r, T, S, nodes, cnt)) {
         }
     best = T.best;
 }

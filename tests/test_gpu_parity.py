@@ -106,3 +106,18 @@ def test_sponza_full_frame_pixels_vs_oracle(gpu, oracle):
     for p in rng.choice(W * H, 48, replace=False):
         ref, _, _ = oracle.render(arrays, S, int(p), int(p) + 1, threads=1)
         assert np.array_equal(rtref.bits(out[p]), rtref.bits(ref[0])), f"pixel {p}"
+
+
+@pytest.mark.parametrize("compact_below,groups", [("0", "1"), ("2", "1"), ("0.9", "2"), ("0.5", "3")])
+def test_wavefront_queue_modes(gpu, monkeypatch, compact_below, groups):
+    """The wavefront path with its dense queue kept to the end (0), compacted from the first
+    check (2), and switched part-way, with 1-3 slot groups on separate streams: same bits
+    and counters as the reference (RT_WF_* are read when a scene is uploaded)."""
+    monkeypatch.setenv("RT_WF_COMPACT_BELOW", compact_below)
+    monkeypatch.setenv("RT_WF_GROUPS", groups)
+    name, w, h, s = "sponza_mini", 64, 36, 4
+    scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
+    out, st = _sums(scene, s, count=True, kernel=0)
+    g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
+    assert np.array_equal(rtref.bits(out), rtref.bits(g["sums"].reshape(-1, 3)))
+    assert st["rays"] == int(g["counters"][0]) and st["aabb_tests"] == int(g["counters"][1])
