@@ -48,7 +48,8 @@ struct rt_device_scene {
     int wf_refill = 8;
     int wf_chunk = 64;
     int wf_node_lds = 0;  // top BVH levels in LDS (RT_WF_NODE_LDS)
-    double wf_compact_below = 0.5;  // dense queue until this fraction of slots is active (RT_WF_COMPACT_BELOW)
+    double wf_compact_below = 0.75;
+    int wf_policy = 0, wf_node_cost = 150, wf_leaf_cost = 85;   // RT_WF_PHASE_POLICY, RT_WF_NODE_COST, RT_WF_LEAF_COST  // dense queue until this fraction of slots is active (RT_WF_COMPACT_BELOW)
     int wf_ext_bpc = 0;   // 0 = as many as fit
 };
 
@@ -191,7 +192,8 @@ template <bool COUNT, bool NODE_LDS>
 __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float4 *qin, const unsigned *count,
                                                          unsigned npos, float4 *hits, unsigned *fetch,
                                                          unsigned *next_count, unsigned long long *counters, int refill,
-                                                         unsigned chunk) {
+                                                         unsigned chunk, int policy, int policy_node_cost,
+                                                         int policy_leaf_cost) {
     const unsigned n = npos ? npos : *count;   // queue positions (dense: all slots of the group)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
@@ -243,7 +245,18 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
                 }
             }
         }
-        if (busy && rtd::trav_step<COUNT>(sc, r, T, S, nodes, cnt)) {
+        // phase choice: lanes at internal nodes and lanes at leaf triangles run different
+        // code; with policy != 0 a wave runs only one of the two per iteration (the one with
+        // more useful lanes per instruction) and the other lanes wait, instead of paying for
+        // both branches every iteration.
+        bool step = busy;
+        if (policy) {
+            const int nn = __popcll(__ballot(busy && T.phase == rtd::TP_NODE));
+            const int nl = __popcll(__ballot(busy && T.phase == rtd::TP_LEAF));
+            const bool do_node = nn * policy_leaf_cost >= nl * policy_node_cost;
+            step = busy && ((T.phase == rtd::TP_NODE) == do_node);
+        }
+        if (step && rtd::trav_step<COUNT>(sc, r, T, S, nodes, cnt)) {
             rtd::store_hit(hits, q, T.best);
             busy = false;
         }
@@ -431,6 +444,9 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_WF_CHUNK")) d->wf_chunk = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_WF_NODE_LDS")) d->wf_node_lds = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_WF_COMPACT_BELOW")) d->wf_compact_below = std::atof(e);
+    if (const char *e = std::getenv("RT_WF_PHASE_POLICY")) d->wf_policy = std::atoi(e);
+    if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
+    if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
     if (const char *e = std::getenv("RT_WF_EXTEND_BLOCKS_PER_CU")) d->wf_ext_bpc = std::max(0, std::atoi(e));
     uint8_t *b = (uint8_t *)d->buf;
@@ -592,7 +608,7 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
             unsigned *c = &d->wf_count[4 * k];
             HIP_TRY(timer.mark(0, sk));
             const unsigned npos = dense[k] ? (unsigned)(hi[k] - lo[k]) : 0u;
-            hipLaunchKernelGGL(extend, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], npos, hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk);
+            hipLaunchKernelGGL(extend, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], npos, hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk, d->wf_policy, d->wf_node_cost, d->wf_leaf_cost);
             HIP_TRY(timer.mark(0, sk));
             HIP_TRY(timer.mark(1, sk));
             auto shade = count ? (mat_lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
