@@ -39,7 +39,8 @@ struct rt_device_scene {
     rtd::WfState wf{};
     float4 *wf_queue[2] = {nullptr, nullptr};
     float4 *wf_hits = nullptr;
-    unsigned *wf_count = nullptr;       // per slot group: [4k] [4k+1] queue counts, [4k+2] extend ray counter
+    unsigned *wf_count = nullptr;       // per slot group: [4k] [4k+1] queue counts (active rays)
+    unsigned *wf_fetch = nullptr;       // per slot group: kParts extend claim counters
     unsigned *wf_host_count = nullptr;  // pinned, per group
     int wf_groups = 1;                  // slot groups, each on its own stream (RT_WF_GROUPS)
     hipStream_t wf_stream[kMaxGroups] = {};
@@ -49,7 +50,8 @@ struct rt_device_scene {
     int wf_chunk = 64;
     int wf_node_lds = 0;  // top BVH levels in LDS (RT_WF_NODE_LDS)
     double wf_compact_below = 0.75;
-    int wf_policy = 0, wf_node_cost = 150, wf_leaf_cost = 85;   // RT_WF_PHASE_POLICY, RT_WF_NODE_COST, RT_WF_LEAF_COST  // dense queue until this fraction of slots is active (RT_WF_COMPACT_BELOW)
+    int wf_policy = 0, wf_node_cost = 150, wf_leaf_cost = 85;
+    int wf_xcd = 0;   // XCD-affine queue parts in extend (RT_WF_XCD; measured slower, off)   // RT_WF_PHASE_POLICY, RT_WF_NODE_COST, RT_WF_LEAF_COST  // dense queue until this fraction of slots is active (RT_WF_COMPACT_BELOW)
     int wf_ext_bpc = 0;   // 0 = as many as fit
 };
 
@@ -188,12 +190,13 @@ __global__ void __launch_bounds__(256) wf_init_kernel(DevScene sc, ShardGeom g, 
 // queue; a wave claims a new chunk of `chunk` entries with one atomic when its chunk runs
 // out (a single shared counter hit by every refill serialises all waves on one address).
 // The rays sit in the queue entries: one coalesced load each.
+constexpr unsigned kParts = 8;   // extend queue parts (XCDs)
 template <bool COUNT, bool NODE_LDS>
 __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float4 *qin, const unsigned *count,
                                                          unsigned npos, float4 *hits, unsigned *fetch,
                                                          unsigned *next_count, unsigned long long *counters, int refill,
                                                          unsigned chunk, int policy, int policy_node_cost,
-                                                         int policy_leaf_cost) {
+                                                         int policy_leaf_cost, int xcd_parts) {
     const unsigned n = npos ? npos : *count;   // queue positions (dense: all slots of the group)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&counters[7], (unsigned long long)n);  // rays extended
@@ -208,6 +211,12 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
     const Nodes nodes{sc.node};
     const rtd::NodeRec root = rtd::load_node(sc.node, 0);
     unsigned q = 0, lo = 0, hi = 0;   // [lo, hi): the wave's unclaimed part of its chunk
+    // XCD affinity: the queue is cut into kParts contiguous parts (dense queue = pixel bands);
+    // blocks sharing an XCD (blockIdx % 8, MI355X_MICROARCH.md) drain their own part first,
+    // so an XCD's L2 holds the BVH region of its band's rays, then help the other parts.
+    const unsigned home = xcd_parts ? blockIdx.x % kParts : 0;
+    unsigned part_i = 0;   // parts tried so far, in order home, home+1, ...
+    const unsigned nparts = xcd_parts ? kParts : 1;
     bool busy = false, exhausted = false;
     rtd::Ray r;
     rtd::TravState T;
@@ -219,15 +228,24 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
             unsigned got = 0, mine = 0xffffffffu;
             while (got < idle) {
                 if (lo >= hi) {
-                    unsigned b = 0;
-                    if (lane == 0) b = atomicAdd(fetch, chunk);
-                    b = __shfl(b, 0, 64);
-                    if (b >= n) {
+                    while (part_i < nparts) {
+                        const unsigned part = (home + part_i) % nparts;
+                        const unsigned p0 = (unsigned)((unsigned long long)n * part / nparts);
+                        const unsigned p1 = (unsigned)((unsigned long long)n * (part + 1) / nparts);
+                        unsigned b = 0;
+                        if (lane == 0) b = atomicAdd(&fetch[part], chunk);
+                        b = __shfl(b, 0, 64);
+                        if (p0 + b < p1) {
+                            lo = p0 + b;
+                            hi = lo + chunk < p1 ? lo + chunk : p1;
+                            break;
+                        }
+                        ++part_i;
+                    }
+                    if (part_i >= nparts) {
                         exhausted = true;
                         break;
                     }
-                    lo = b;
-                    hi = b + chunk < n ? b + chunk : n;
                 }
                 const unsigned k = hi - lo < idle - got ? hi - lo : idle - got;
                 if (!busy && rank >= got && rank < got + k) mine = lo + (rank - got);
@@ -297,7 +315,7 @@ __global__ void __launch_bounds__(256) wf_shade_kernel(DevScene sc_in, ShardGeom
         sc.mesh_nt = L.nt;
     }
     const unsigned n = npos ? npos : *cin;   // input positions (dense: all slots of the group)
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fetch = 0;   // the next extend launch's ray counter
+    if (blockIdx.x == 0 && threadIdx.x < kParts) fetch[threadIdx.x] = 0;   // the next extend launch's ray counters
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     for (unsigned base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const unsigned q = base + threadIdx.x;
@@ -445,6 +463,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_WF_NODE_LDS")) d->wf_node_lds = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_WF_COMPACT_BELOW")) d->wf_compact_below = std::atof(e);
     if (const char *e = std::getenv("RT_WF_PHASE_POLICY")) d->wf_policy = std::atoi(e);
+    if (const char *e = std::getenv("RT_WF_XCD")) d->wf_xcd = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -493,6 +512,7 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     const size_t bytes = (size_t)cap * 4 * (size_t)planes;
     HIP_TRY(hipMalloc(&d->wf_buf, bytes));
     HIP_TRY(hipMalloc((void **)&d->wf_count, 16 * kMaxGroups));
+    if (!d->wf_fetch) HIP_TRY(hipMalloc((void **)&d->wf_fetch, sizeof(unsigned) * kParts * kMaxGroups));
     HIP_TRY(hipHostMalloc((void **)&d->wf_host_count, 16 * kMaxGroups, hipHostMallocDefault));
     for (int k = 0; k < d->wf_groups; ++k)
         if (!d->wf_stream[k]) HIP_TRY(hipStreamCreateWithFlags(&d->wf_stream[k], hipStreamNonBlocking));
@@ -571,6 +591,7 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
     w.n = g.n_pixels;
     const int G = (int)std::min<long long>(d->wf_groups, std::max<long long>(1, g.n_pixels / 4096));
     HIP_TRY(hipMemsetAsync(d->wf_count, 0, 16 * kMaxGroups, stream));
+    HIP_TRY(hipMemsetAsync(d->wf_fetch, 0, sizeof(unsigned) * kParts * kMaxGroups, stream));
     HIP_TRY(hipEventRecord(d->wf_event[G], stream));
     long long lo[kMaxGroups], hi[kMaxGroups];
     bool live[kMaxGroups], dense[kMaxGroups], to_compact[kMaxGroups];
@@ -606,15 +627,16 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
             float4 *qi = d->wf_queue[cur] + rtd::kQRec * lo[k], *qo = d->wf_queue[1 - cur] + rtd::kQRec * lo[k];
             float4 *hits = d->wf_hits + lo[k];
             unsigned *c = &d->wf_count[4 * k];
+            unsigned *fetch = &d->wf_fetch[kParts * k];
             HIP_TRY(timer.mark(0, sk));
             const unsigned npos = dense[k] ? (unsigned)(hi[k] - lo[k]) : 0u;
-            hipLaunchKernelGGL(extend, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], npos, hits, &c[2], &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk, d->wf_policy, d->wf_node_cost, d->wf_leaf_cost);
+            hipLaunchKernelGGL(extend, dim3(ext_blocks), dim3(256), 0, sk, d->ds, qi, &c[cur], npos, hits, fetch, &c[1 - cur], d->counters, d->wf_refill, (unsigned)d->wf_chunk, d->wf_policy, d->wf_node_cost, d->wf_leaf_cost, d->wf_xcd);
             HIP_TRY(timer.mark(0, sk));
             HIP_TRY(timer.mark(1, sk));
             auto shade = count ? (mat_lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
                                : (mat_lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
             const int dense_out = dense[k] && !to_compact[k];
-            hipLaunchKernelGGL(shade, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], npos, hits, qo, &c[1 - cur], (long long)lo[k], dense_out, &c[2], d_out, d->counters);
+            hipLaunchKernelGGL(shade, dim3(sh_blocks), dim3(256), 0, sk, d->ds, g, w, spp, qi, &c[cur], npos, hits, qo, &c[1 - cur], (long long)lo[k], dense_out, fetch, d_out, d->counters);
             if (to_compact[k]) dense[k] = false;
             HIP_TRY(timer.mark(1, sk));
         }
@@ -737,6 +759,7 @@ void rt_device_scene_release(rt_scene *s) {
         if (d->queue) (void)hipFree(d->queue);
         if (d->wf_buf) (void)hipFree(d->wf_buf);
         if (d->wf_count) (void)hipFree(d->wf_count);
+        if (d->wf_fetch) (void)hipFree(d->wf_fetch);
         if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
         for (hipStream_t &x : d->wf_stream)
             if (x) (void)hipStreamDestroy(x);
