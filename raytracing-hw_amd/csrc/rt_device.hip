@@ -45,14 +45,15 @@ struct rt_device_scene {
     int wf_groups = 1;                  // slot groups, each on its own stream (RT_WF_GROUPS)
     hipStream_t wf_stream[kMaxGroups] = {};
     hipEvent_t wf_event[kMaxGroups + 1] = {};
-    // tuning (RT_WF_REFILL, RT_WF_CHUNK, RT_WF_EXTEND_BLOCKS_PER_CU environment overrides, read at upload)
-    int wf_refill = 8;
-    int wf_chunk = 64;
-    int wf_node_lds = 0;  // top BVH levels in LDS (RT_WF_NODE_LDS)
-    double wf_compact_below = 0.75;
-    int wf_policy = 0, wf_node_cost = 150, wf_leaf_cost = 85;
-    int wf_xcd = 0;   // XCD-affine queue parts in extend (RT_WF_XCD; measured slower, off)   // RT_WF_PHASE_POLICY, RT_WF_NODE_COST, RT_WF_LEAF_COST  // dense queue until this fraction of slots is active (RT_WF_COMPACT_BELOW)
-    int wf_ext_bpc = 0;   // 0 = as many as fit
+    // tuning knobs, environment overrides read at upload (measured values in DESIGN.md §6):
+    int wf_refill = 8;                 // RT_WF_REFILL: idle lanes before a wave refills
+    int wf_chunk = 64;                 // RT_WF_CHUNK: queue entries claimed per atomic
+    int wf_node_lds = 0;               // RT_WF_NODE_LDS: top BVH levels in LDS (measured: no gain)
+    double wf_compact_below = 0.75;    // RT_WF_COMPACT_BELOW: dense queue until this active fraction
+    int wf_policy = 0;                 // RT_WF_PHASE_POLICY: one of node/leaf steps per iteration (slower)
+    int wf_node_cost = 150, wf_leaf_cost = 85;   // RT_WF_NODE_COST / RT_WF_LEAF_COST for that policy
+    int wf_xcd = 0;                    // RT_WF_XCD: XCD-affine queue parts in extend (measured slower)
+    int wf_ext_bpc = 0;                // RT_WF_EXTEND_BLOCKS_PER_CU: 0 = as many as fit
 };
 
 #define HIP_TRY(expr)                                                                          \
