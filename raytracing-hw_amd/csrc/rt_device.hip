@@ -19,6 +19,7 @@
 #include "rt_path.h"
 #include "rt_wave.h"
 #include "rt_wavefront.h"
+#include "rt_mega.h"
 #include "rt_scene.h"
 
 using rtd::Counters;
@@ -54,6 +55,7 @@ struct rt_device_scene {
     int wf_node_cost = 150, wf_leaf_cost = 85;   // RT_WF_NODE_COST / RT_WF_LEAF_COST for that policy
     int wf_xcd = 0;                    // RT_WF_XCD: XCD-affine queue parts in extend (measured slower)
     int wf_ext_bpc = 0;                // RT_WF_EXTEND_BLOCKS_PER_CU: 0 = as many as fit
+    int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 4 shades once this many lanes are ready
 };
 
 #define HIP_TRY(expr)                                                                          \
@@ -162,6 +164,49 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
         if (L.state == rtd::L_TRAV) L.state = rtd::L_SHADE;
         // (D) shade, bounce or end the path
         if (L.state == rtd::L_SHADE) rtd::lane_shade<COUNT>(L, sc, spp, out, cnt);
+    }
+    flush_counters<COUNT>(cnt, counters);
+}
+
+// ------------------------------------------------------------------------ lane-resident (kernel 4)
+// rt_mega.h: every lane runs whole pixels; traversal one unit per iteration, shading batched
+// per wave (READY lanes wait for `shade_min` of them or for no lane left traversing).
+template <bool COUNT>
+__global__ void __launch_bounds__(256) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
+                                                       unsigned long long *counters, unsigned int *queue,
+                                                       int shade_min) {
+    const int lane = threadIdx.x & 63;
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    uint2 spill[rtd::kStack - rtd::kLdsStack];
+    rtd::LdsStack S{spill};
+    const rtd::GlobalNodes nodes{sc.node};
+    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
+    rtd::MegaLane L;
+    L.pix = -1;
+    L.state = rtd::M_IDLE;
+    bool exhausted = false;
+    for (;;) {
+        if (!exhausted) {   // lanes without a pixel take the next ones (one atomic per wave)
+            const bool need = L.pix < 0;
+            const unsigned long long m = __ballot(need);
+            if (m) {
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                const unsigned cm = (unsigned)__popcll(m);
+                unsigned base = 0;
+                if (lane == leader) base = atomicAdd(queue, cm);
+                base = __shfl(base, leader, 64);
+                if (need) {
+                    const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
+                    if (p < g.n_pixels) rtd::mega_assign<COUNT>(L, sc, g, p, root, cnt);
+                }
+                if ((long long)base + cm >= g.n_pixels) exhausted = true;
+            }
+        }
+        if (!__any(L.pix >= 0)) break;
+        const int nr = __popcll(__ballot(L.state == rtd::M_READY));
+        const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
+        const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
+        rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, root, S, nodes, cnt);
     }
     flush_counters<COUNT>(cnt, counters);
 }
@@ -465,6 +510,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_WF_COMPACT_BELOW")) d->wf_compact_below = std::atof(e);
     if (const char *e = std::getenv("RT_WF_PHASE_POLICY")) d->wf_policy = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_XCD")) d->wf_xcd = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -705,6 +751,21 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
         } else if (p->kernel == 0) {
             int rc = launch_wavefront(d, g, spp, s->ray_depth, d_out, stream, count, timer);
             if (rc) return rc;
+        } else if (p->kernel == 4) {
+            if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "kernel 4: ray_depth must be in [1, 15]");
+            int rc = ensure_wf(d, g.n_pixels, s->ray_depth);   // vertex records
+            if (rc) return rc;
+            rtd::WfState w = d->wf;
+            w.n = g.n_pixels;
+            auto mk = count ? rt_mega_kernel<true> : rt_mega_kernel<false>;
+            int per_cu = 0;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk, 256, 0));
+            if (per_cu < 1) per_cu = 1;
+            const long long need = (g.n_pixels + 255) / 256;
+            unsigned blocks = (unsigned)std::min<long long>(need, (long long)d->cu_count * per_cu);
+            if (blocks == 0) blocks = 1;
+            hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
+                               d->mega_shade_min);
         } else {
             // persistent wave kernel: exactly the resident blocks (occupancy query), capped by the work
             int per_cu = 0;

@@ -1,0 +1,106 @@
+// rt_mega.h — lane-resident path tracer for small shards (kernel 4).
+//
+// The wavefront (rt_wavefront.h) advances every path one bounce per launch pair, so each
+// iteration costs as much as the slowest ray of the whole frame; with few paths per GPU
+// (a 1080p frame split over 8 GPUs leaves ~260 k pixels each, about one per lane) the
+// frame time becomes the sum over ~1500 iterations of that maximum.  Here every lane owns
+// one pixel at a time and runs its whole sample loop (scene.cpp:34-42) itself, so a path
+// only ever waits for its own rays:
+//   * traversal advances every traversing lane of a wave by one unit per iteration
+//     (trav_step: one node pair or one triangle, as in the extend kernel);
+//   * lanes whose closest hit is known wait (READY) until `shade_min` lanes of the wave are
+//     ready, or no lane is traversing, and are then shaded together (one pass of the long
+//     shading code serves many lanes);
+//   * a lane whose pixel has all its samples takes the next pixel from a per-launch queue.
+// RNG, pixel sum, sample counter and depth budget live in registers; the vertex records go
+// to HBM (AosRec, indexed by pixel).  Same per-pixel arithmetic, so bit-identical output.
+#pragma once
+#include "rt_wavefront.h"
+
+namespace rtd {
+
+enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2 };
+
+struct MegaLane {
+    long long pix;   // shard pixel (slot), -1 = none
+    int s, power, nv, state;
+    Rng rng;
+    V3 sum;
+    Ray r;
+    TravState T;
+};
+
+// Closest-hit query start for L.r: BVH::intersect's counters and root box (bvh.cpp:239-243).
+template <bool COUNT>
+__device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Counters &cnt) {
+    float e;
+    const bool hit = box_hit<false>(root.mn, root.mx, L.r, e);
+    const uint32_t bits = (L.r.d.x > 0 ? 1u : 0u) | (L.r.d.y > 0 ? 2u : 0u) | (L.r.d.z > 0 ? 4u : 0u) | (hit ? 0u : 8u);
+    L.state = trav_start<COUNT>(bits, root.a, root.b, L.T, cnt) ? M_TRAV : M_READY;
+}
+
+// Next sample of the lane's pixel: jittered camera ray (scene.cpp:36-39).
+template <bool COUNT>
+__device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
+                                            Counters &cnt) {
+    L.r = start_sample(sc, g, L.pix, L.rng, L.power);
+    L.nv = 0;
+    mega_begin<COUNT>(L, root, cnt);
+}
+
+// A new pixel: seed its RNG (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1), first sample.
+template <bool COUNT>
+__device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, const ShardGeom &g, long long p,
+                                            const NodeRec &root, Counters &cnt) {
+    L.pix = p;
+    L.s = 0;
+    L.sum = V3{0.f, 0.f, 0.f};
+    const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
+    const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
+    L.rng = Rng{seed == 0 ? 1u : seed, 0u, 0.f};
+    mega_sample<COUNT>(L, sc, g, root, cnt);
+}
+
+// Shade the lane's closest hit (one vertex of scene.cpp:85-154); bounce, or end the path:
+// fold, accumulate, next sample or pixel done.
+template <bool COUNT>
+__device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
+                                           int spp, float *out, const NodeRec &root, Counters &cnt) {
+    AosRec P{st.rec_ab, st.rec_c, L.pix, st.D, V3{0.f, 0.f, 0.f}, 0, false};
+    const Hit h = L.T.best;
+    bool next = false;
+    if (h.prim >= 0 && h.t < sc.max_distance && shade_hit<COUNT>(sc, L.r, h, L.rng, cnt, P, L.nv) && L.power > 0) {
+        L.power -= 1;
+        next = true;
+    }
+    P.flush_e();
+    if (next) {
+        mega_begin<COUNT>(L, root, cnt);
+        return;
+    }
+    L.sum = rtv::add(L.sum, fold_path(P, L.nv));
+    if (++L.s == spp) {
+        out[3 * L.pix + 0] = L.sum.x;
+        out[3 * L.pix + 1] = L.sum.y;
+        out[3 * L.pix + 2] = L.sum.z;
+        L.pix = -1;
+        L.state = M_IDLE;
+        return;
+    }
+    mega_sample<COUNT>(L, sc, g, root, cnt);
+}
+
+// One iteration of a wave's main loop for one lane, given the wave's decision: shade the
+// READY lanes this iteration (shade_now), or step the traversing lanes.
+template <bool COUNT, class Stack, class Nodes>
+__device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
+                                             const WfState &st, int spp, float *out, const NodeRec &root, Stack &stk,
+                                             const Nodes &nodes, Counters &cnt) {
+    if (shade_now) {
+        if (L.state == M_READY) mega_shade<COUNT>(L, sc, g, st, spp, out, root, cnt);
+    } else if (L.state == M_TRAV) {
+        if (trav_step<COUNT>(sc, L.r, L.T, stk, nodes, cnt)) L.state = M_READY;
+    }
+}
+
+}  // namespace rtd

@@ -4,7 +4,7 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
-#include "../../raytracing-hw_amd/csrc/rt_wavefront.h"
+#include "../../raytracing-hw_amd/csrc/rt_mega.h"
 #include "../../include/rt_hw.h"
 
 static rtd::DevScene make(const rt_scene_view *v) {
@@ -210,4 +210,72 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
         else if (kind == 1) out_f[k] = rtd::rng_uniform_m11(rng);
         else out_f[k] = rtd::rng_normal(rng);
     }
+}
+
+// Emulates rt_mega_kernel (kernel 4): `waves` waves of 64 lanes, round-robin one main-loop
+// iteration at a time, sharing the pixel queue, with the kernel's shade_min decision.
+extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
+                              int shade_min, float *out, uint64_t *cnt_out) {
+    rtd::DevScene sc = make(v);
+    sc.n_tris = (int)v->n_tris;
+    sc.n_nodes = (int)v->n_nodes;
+    int64_t rows = 0;
+    for (int r = 0; r < v->height; ++r)
+        if ((r / row_block) % world == rank) ++rows;
+    const long long n = (long long)rows * v->width;
+    rtd::ShardGeom g{v->width, rank, world, row_block, n};
+    const int D = v->ray_depth;
+    std::vector<float4> ab((size_t)2 * n * D);
+    std::vector<float> cv((size_t)n * D);
+    rtd::WfState st{};
+    st.n = n;
+    st.D = D;
+    st.rec_ab = ab.data();
+    st.rec_c = cv.data();
+    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
+    const rtd::GlobalNodes nodes{sc.node};
+    std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
+    std::vector<std::vector<uint2>> stacks((size_t)waves * 64, std::vector<uint2>(rtd::kStack));
+    for (auto &L : lanes) { L.pix = -1; L.state = rtd::M_IDLE; }
+    std::vector<char> exhausted(waves, 0), done(waves, 0);
+    rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    long long queue = 0;
+    int live = waves;
+    while (live > 0) {
+        for (int w = 0; w < waves; ++w) {
+            if (done[w]) continue;
+            rtd::MegaLane *W = &lanes[(size_t)w * 64];
+            if (!exhausted[w]) {
+                uint64_t m = 0;
+                for (int l = 0; l < 64; ++l) if (W[l].pix < 0) m |= 1ull << l;
+                if (m) {
+                    const long long base = queue;
+                    const int cm = __builtin_popcountll(m);
+                    queue += cm;
+                    for (int l = 0; l < 64; ++l) {
+                        if (!(m >> l & 1)) continue;
+                        const long long p = base + __builtin_popcountll(m & ((1ull << l) - 1ull));
+                        if (p < n) rtd::mega_assign<true>(W[l], sc, g, p, root, cnt);
+                    }
+                    if (base + cm >= n) exhausted[w] = 1;
+                }
+            }
+            bool any = false;
+            int nr = 0, nt = 0;
+            for (int l = 0; l < 64; ++l) {
+                any |= W[l].pix >= 0;
+                nr += W[l].state == rtd::M_READY;
+                nt += W[l].state == rtd::M_TRAV;
+            }
+            if (!any) { done[w] = 1; --live; continue; }
+            const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
+            for (int l = 0; l < 64; ++l) {
+                rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
+                rtd::mega_iterate<true>(W[l], shade_now, sc, g, st, spp, out, root, S, nodes, cnt);
+            }
+        }
+    }
+    uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
+    std::memcpy(cnt_out, c, sizeof c);
+    return 0;
 }

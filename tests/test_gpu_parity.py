@@ -27,7 +27,7 @@ def _sums(scene, spp, **kw):
     return out.reshape(-1, 3), st
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("name,w,h,s", CASES)
 def test_sums_match_reference(gpu, name, w, h, s, kernel):
     scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))

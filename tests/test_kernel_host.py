@@ -37,6 +37,8 @@ def kh(tmp_path_factory):
     lib.kh_render_wave.restype = I
     lib.kh_render_wf.argtypes = [V, I, I, I, I, V, V, V]
     lib.kh_render_wf.restype = I
+    lib.kh_render_mega.argtypes = [V, I, I, I, I, I, I, V, V]
+    lib.kh_render_mega.restype = I
     return lib
 
 
@@ -136,3 +138,17 @@ def test_rng_sequences_match_reference(kh):
         assert np.array_equal(rtref.bits(f), rtref.bits(g["raw_uniform"][row]))
         kh.kh_rng(seed, 2, 8, f.ctypes.data, u.ctypes.data)
         assert np.array_equal(rtref.bits(f), rtref.bits(g["raw_normal"][row]))
+
+
+@pytest.mark.parametrize("name,w,h,s,waves,shade_min", [("cornell_blob", 48, 48, 4, 2, 32), ("sponza_mini", 64, 36, 4, 3, 1),
+                                                        ("cornell", 33, 17, 3, 1, 64)])
+def test_lane_resident_emulation(rt, kh, name, w, h, s, waves, shade_min):
+    """Kernel 4 (rt_mega.h): lanes own whole pixels, traversal steps per iteration, batched
+    shading; bit-exact sums and counters."""
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    out = np.zeros((h * w, 3), np.float32)
+    cnt = np.zeros(7, np.uint64)
+    assert kh.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data, cnt.ctypes.data) == 0
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert list(cnt[:6]) == list(cnt_want)
