@@ -9,11 +9,13 @@ followed by the RCCL all-gather of the float framebuffer.  Rank 0 prints one JSO
 
 value    = scene closest-hit queries (rays, counted in-kernel during warmup; the count is
            deterministic per frame) of all ranks x K / max-over-ranks wall time of the K steps
-roofline = the dominant kernel of rank 0 (wf_extend, the BVH traversal): algorithmic bytes
-           per launch (24 B per AABB test + 36 B per triangle test + 44 B of ray/hit I/O per
-           ray) / its average launch duration (HIP events around every launch in
-           the timed steps), against the 8 TB/s HBM3E peak.  path_* = the whole-path model
-           of SURVEY.md §8d (scene + light BVH + 156 B per shaded hit) over the frame time.
+roofline = rank 0's render kernel.  Default (kernel 0, lane-resident rt_mega_kernel): one
+           launch renders the frame, so achieved = the algorithmic bytes of the whole path
+           (24 B per AABB test + 36 B per triangle test, scene and light BVH,
+           + 156 B per shaded hit) / that launch's duration (HIP events on the launch stream).
+           With --kernel 4 (wavefront) it is the extend kernel alone: 24 B per AABB test +
+           36 B per triangle test + 44 B of ray/hit I/O per ray, per launch / its average
+           duration.  Peak: 8 TB/s HBM3E.
 cpu_baseline: the reference itself (oracle/_ref/ref_harness, built from /root/reference's
            sources) timing Scene::render on the host cores over a bounded sample of the same
            frame; falls back to the build's CPU restatement (oracle/) when _ref is absent.
@@ -99,7 +101,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--kernel", type=int, default=0, help="0 wavefront (default), 1 one lane per pixel, 2 persistent per pixel, 3 wave megakernel")
+    ap.add_argument("--kernel", type=int, default=0, help="0 lane-resident (default), 1 one lane per pixel, "
+                    "2 persistent per pixel, 3 wave megakernel, 4 wavefront")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the frame in the CPU baseline sample")
     ap.add_argument("--cpu-spp", type=int, default=1)
@@ -186,7 +189,7 @@ def main():
         bytes_frame = (B_AABB * (c0["aabb_tests"] + c0["light_aabb_tests"]) + B_TRI * (c0["tri_tests"] + c0["light_tri_tests"])
                        + B_SHADE * c0["shading_hits"])
         frame_s = float(np.mean(kernel_ms)) / 1e3
-        if args.kernel == 0 and sum(ext_n) > 0:
+        if args.kernel == 4 and sum(ext_n) > 0:
             # dominant kernel = wf_extend: scene-BVH node pairs + triangles + per-ray SoA in/out
             ext_bytes = B_AABB * c0["aabb_tests"] + B_TRI * c0["tri_tests"] + B_RAY_IO * ext_rays[0]
             launches = float(np.mean(ext_n))
@@ -194,7 +197,9 @@ def main():
             avg_s = float(np.sum(ext_ms)) / float(np.sum(ext_n)) / 1e3
             kname = "wf_extend_kernel"
         else:
-            bytes_launch, avg_s, launches, kname = bytes_frame, frame_s, 1.0, "render kernel"
+            # one launch renders the frame: the whole-path model over the launch time
+            bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
+            kname = ["rt_mega_kernel", "rt_pixels_kernel", "rt_persistent_kernel", "rt_wave_kernel"][args.kernel]
         achieved = bytes_launch / avg_s / 1e9
         line = {
             "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",
@@ -212,7 +217,7 @@ def main():
                     "procedural RGBA8 textures; SURVEY.md App. C)",
             "config": {"workload": f"{args.scene} proxy {W}x{H}x{S}spp depth 6, one frame per step",
                        "scene": args.scene, "width": W, "height": H, "spp": S, "triangles": int(n_tris),
-                       "kernel": ["wavefront", "pixel", "persistent-pixel", "wave"][args.kernel], "parallelism": f"pixel-rows x{world}",
+                       "kernel": ["lane-resident", "pixel", "persistent-pixel", "wave", "wavefront"][args.kernel], "parallelism": f"pixel-rows x{world}",
                        "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
                        "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 3)},

@@ -85,13 +85,14 @@ typedef struct {
     int32_t rank, world;  /* pixel-row partition: rows whose (row / row_block) % world == rank */
     int32_t row_block;    /* rows per interleave block (default 8)                       */
     int32_t count;        /* 1 = accumulate ray / AABB / triangle test counters          */
-    int32_t kernel;       /* 0 = wavefront (default), 1 = one lane per pixel, 2 = persistent per-pixel, 3 = wave megakernel */
+    int32_t kernel;       /* 0 = lane-resident (default), 1 = one lane per pixel, 2 = persistent per-pixel,
+                             3 = wave megakernel, 4 = wavefront (extend/shade launches) */
     int32_t flags;        /* RT_FLAG_* */
     int32_t reserved;
 } rt_params;
 
 /* rt_params.flags */
-#define RT_FLAG_KERNEL_TIMES 1  /* wavefront path: time every extend / shade launch (HIP events) */
+#define RT_FLAG_KERNEL_TIMES 1  /* wavefront path (kernel 4): time every extend / shade launch (HIP events) */
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */

@@ -748,11 +748,11 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (blocks == 0) blocks = 1;
             if (count) hipLaunchKernelGGL(rt_persistent_kernel<true>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
             else hipLaunchKernelGGL(rt_persistent_kernel<false>, dim3(blocks), dim3(256), 0, stream, d->ds, g, spp, d_out, d->counters, d->queue);
-        } else if (p->kernel == 0) {
+        } else if (p->kernel == 4) {
             int rc = launch_wavefront(d, g, spp, s->ray_depth, d_out, stream, count, timer);
             if (rc) return rc;
-        } else if (p->kernel == 4) {
-            if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "kernel 4: ray_depth must be in [1, 15]");
+        } else if (p->kernel == 0) {   // lane-resident (rt_mega.h), the default
+            if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "ray_depth must be in [1, 15]");
             int rc = ensure_wf(d, g.n_pixels, s->ray_depth);   // vertex records
             if (rc) return rc;
             rtd::WfState w = d->wf;

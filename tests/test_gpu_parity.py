@@ -66,16 +66,17 @@ def test_rays_match_reference(gpu, name):
     assert np.array_equal(i[:, 5], g["n_light_tri"].astype(np.int64))
 
 
+@pytest.mark.parametrize("kernel", [0, 4])
 @pytest.mark.parametrize("world", [2, 3, 8])
-def test_partition_invariance(gpu, world):
+def test_partition_invariance(gpu, world, kernel):
     """Row-block shards (the multi-GPU partition) reassemble to the single-shard frame."""
     w, h, s = 40, 70, 2
     scene = gpu.Scene.load(rtref.scene_path("sponza_mini"), w, h, s)
-    full, _ = scene.render_sums(s)
+    full, _ = scene.render_sums(s, kernel=kernel)
     frame = np.zeros_like(full)
     for rank in range(world):
         rows = gpu.shard_rows(h, rank, world, 8)
-        part, _ = scene.render_sums(s, rank=rank, world=world, row_block=8)
+        part, _ = scene.render_sums(s, rank=rank, world=world, row_block=8, kernel=kernel)
         frame[rows] = part
     assert np.array_equal(rtref.bits(frame), rtref.bits(full))
 
@@ -117,7 +118,7 @@ def test_wavefront_queue_modes(gpu, monkeypatch, compact_below, groups):
     monkeypatch.setenv("RT_WF_GROUPS", groups)
     name, w, h, s = "sponza_mini", 64, 36, 4
     scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
-    out, st = _sums(scene, s, count=True, kernel=0)
+    out, st = _sums(scene, s, count=True, kernel=4)
     g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
     assert np.array_equal(rtref.bits(out), rtref.bits(g["sums"].reshape(-1, 3)))
     assert st["rays"] == int(g["counters"][0]) and st["aabb_tests"] == int(g["counters"][1])
