@@ -55,7 +55,8 @@ struct rt_device_scene {
     int wf_node_cost = 150, wf_leaf_cost = 85;   // RT_WF_NODE_COST / RT_WF_LEAF_COST for that policy
     int wf_xcd = 0;                    // RT_WF_XCD: XCD-affine queue parts in extend (measured slower)
     int wf_ext_bpc = 0;                // RT_WF_EXTEND_BLOCKS_PER_CU: 0 = as many as fit
-    int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 4 shades once this many lanes are ready
+    int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
+    int mega_wpe = 5;                  // RT_MEGA_WPE: minimum waves per SIMD the register allocation targets
 };
 
 #define HIP_TRY(expr)                                                                          \
@@ -171,8 +172,8 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
 // ------------------------------------------------------------------------ lane-resident (kernel 4)
 // rt_mega.h: every lane runs whole pixels; traversal one unit per iteration, shading batched
 // per wave (READY lanes wait for `shade_min` of them or for no lane left traversing).
-template <bool COUNT>
-__global__ void __launch_bounds__(256) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
+template <bool COUNT, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
                                                        int shade_min) {
     const int lane = threadIdx.x & 63;
@@ -511,6 +512,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_WF_PHASE_POLICY")) d->wf_policy = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_XCD")) d->wf_xcd = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("RT_MEGA_WPE")) d->mega_wpe = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -757,7 +759,15 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (rc) return rc;
             rtd::WfState w = d->wf;
             w.n = g.n_pixels;
-            auto mk = count ? rt_mega_kernel<true> : rt_mega_kernel<false>;
+            auto pick = [&](int wpe) {
+                switch (wpe) {
+                    case 5: return count ? rt_mega_kernel<true, 5> : rt_mega_kernel<false, 5>;
+                    case 6: return count ? rt_mega_kernel<true, 6> : rt_mega_kernel<false, 6>;
+                    case 8: return count ? rt_mega_kernel<true, 8> : rt_mega_kernel<false, 8>;
+                    default: return count ? rt_mega_kernel<true, 1> : rt_mega_kernel<false, 1>;
+                }
+            };
+            auto mk = pick(d->mega_wpe);
             int per_cu = 0;
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk, 256, 0));
             if (per_cu < 1) per_cu = 1;
