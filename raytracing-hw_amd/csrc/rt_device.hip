@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 #include <cstdlib>
+#include <algorithm>
 #include <type_traits>
 
 #include "rt_path.h"
@@ -57,6 +58,17 @@ struct rt_device_scene {
     int wf_ext_bpc = 0;                // RT_WF_EXTEND_BLOCKS_PER_CU: 0 = as many as fit
     int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
     int mega_wpe = 5;                  // RT_MEGA_WPE: minimum waves per SIMD the register allocation targets
+    int mega_reorder = 1;              // RT_MEGA_REORDER: heaviest-first pixel order from the last counting render
+    int mega_prio = 0;                 // RT_MEGA_PRIO: wave priority levels of this many traversal tests (0 = off)
+    int mega_times = 0;                // RT_MEGA_TIMES: diagnostics, per-pixel finish-time percentiles
+    unsigned long long *mega_tfin = nullptr;
+    long long mega_tfin_n = 0;
+    // that order (per shard geometry): pixel indices by descending traversal work
+    int *order = nullptr;
+    unsigned *order_cost = nullptr;
+    long long order_n = 0, order_cap = 0;
+    int order_key[3] = {0, 0, 0};
+    bool order_valid = false;
 };
 
 #define HIP_TRY(expr)                                                                          \
@@ -175,7 +187,9 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
 template <bool COUNT, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
-                                                       int shade_min) {
+                                                       int shade_min, const int *order, unsigned *cost,
+                                                       const unsigned *prio_cost, unsigned prio_unit,
+                                                       unsigned long long *tfin) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 spill[rtd::kStack - rtd::kLdsStack];
@@ -198,16 +212,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                 base = __shfl(base, leader, 64);
                 if (need) {
                     const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (p < g.n_pixels) rtd::mega_assign<COUNT>(L, sc, g, p, root, cnt);
+                    if (p < g.n_pixels) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : p, root, cnt);
                 }
                 if ((long long)base + cm >= g.n_pixels) exhausted = true;
+                if (prio_cost) {   // waves holding the costliest pixels issue first (s_setprio)
+                    unsigned c = L.pix >= 0 ? prio_cost[L.pix] : 0u;
+                    for (int off = 32; off > 0; off >>= 1) c = max(c, (unsigned)__shfl_xor((int)c, off, 64));
+                    const unsigned lvl = c / prio_unit;
+                    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+                    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+                    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
             }
         }
         if (!__any(L.pix >= 0)) break;
         const int nr = __popcll(__ballot(L.state == rtd::M_READY));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
         const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
-        rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, root, S, nodes, cnt);
+        const long long pix_before = L.pix;
+        rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
+        if (tfin && pix_before >= 0 && L.pix < 0) tfin[pix_before] = wall_clock64();   // diagnostics
     }
     flush_counters<COUNT>(cnt, counters);
 }
@@ -513,6 +538,9 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_WF_XCD")) d->wf_xcd = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_WPE")) d->mega_wpe = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_REORDER")) d->mega_reorder = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_PRIO")) d->mega_prio = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_TIMES")) d->mega_times = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -774,8 +802,77 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const long long need = (g.n_pixels + 255) / 256;
             unsigned blocks = (unsigned)std::min<long long>(need, (long long)d->cu_count * per_cu);
             if (blocks == 0) blocks = 1;
+            // pixel order: heaviest first, from the per-pixel costs of the last counting render of
+            // this shard (the frame's tail is then made of cheap pixels); natural order otherwise
+            // (only with >= 3 pixels per lane: with fewer, every lane starts at once and sorting
+            // only clusters the heavy pixels on the same SIMDs — measured slower at 4 and 8 GPUs)
+            const bool many = g.n_pixels >= 3LL * blocks * 256;
+            const bool same = many && d->order && d->order_n == g.n_pixels && d->order_key[0] == rank &&
+                              d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && d->mega_reorder;
+            unsigned *cost = nullptr;
+            if (count && st && ((d->mega_reorder && many) || d->mega_prio > 0)) {
+                if (d->order_cap < g.n_pixels) {
+                    if (d->order) (void)hipFree(d->order);
+                    if (d->order_cost) (void)hipFree(d->order_cost);
+        if (d->mega_tfin) (void)hipFree(d->mega_tfin);
+                    d->order = nullptr;
+                    d->order_cost = nullptr;
+                    d->order_cap = 0;
+                    HIP_TRY(hipMalloc((void **)&d->order, sizeof(int) * g.n_pixels));
+                    HIP_TRY(hipMalloc((void **)&d->order_cost, sizeof(unsigned) * g.n_pixels));
+                    d->order_cap = g.n_pixels;
+                }
+                cost = d->order_cost;
+            }
+            if (d->mega_times && d->mega_tfin_n < g.n_pixels) {   // RT_MEGA_TIMES: per-pixel finish clocks
+                if (d->mega_tfin) (void)hipFree(d->mega_tfin);
+                HIP_TRY(hipMalloc((void **)&d->mega_tfin, sizeof(unsigned long long) * g.n_pixels));
+                d->mega_tfin_n = g.n_pixels;
+            }
+            unsigned long long t_launch = 0;
+            if (d->mega_times) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                t_launch = 0;
+            }
+            // wave priority from the same per-pixel costs (RT_MEGA_PRIO = cost unit per level, 0 = off)
+            const bool prio_ok = d->mega_prio > 0 && d->order_cost && d->order_n == g.n_pixels && d->order_key[0] == rank &&
+                                 d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && !cost;
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
-                               d->mega_shade_min);
+                               d->mega_shade_min, same ? (const int *)d->order : nullptr, cost,
+                               prio_ok ? (const unsigned *)d->order_cost : nullptr, (unsigned)std::max(1, d->mega_prio),
+                               d->mega_times ? d->mega_tfin : nullptr);
+            HIP_TRY(hipGetLastError());
+            if (d->mega_times) {   // print finish-time percentiles (ms after the first finish) to stderr
+                std::vector<unsigned long long> t(g.n_pixels);
+                HIP_TRY(hipMemcpyAsync(t.data(), d->mega_tfin, sizeof(unsigned long long) * g.n_pixels,
+                                       hipMemcpyDeviceToHost, stream));
+                HIP_TRY(hipStreamSynchronize(stream));
+                std::sort(t.begin(), t.end());
+                int rate_khz = 0;
+                (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, d->device);
+                const double to_ms = rate_khz > 0 ? 1.0 / rate_khz : 1e-5;
+                std::fprintf(stderr, "[mega times] n=%lld wall-clock kHz=%d finish ms:", (long long)g.n_pixels, rate_khz);
+                for (double q : {0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 0.99, 0.999, 1.0}) {
+                    const size_t k = std::min(t.size() - 1, (size_t)(q * (t.size() - 1)));
+                    std::fprintf(stderr, " p%g=%.1f", q * 100, (double)(t[k] - t[0]) * to_ms);
+                }
+                std::fprintf(stderr, "\n");
+                (void)t_launch;
+            }
+            if (cost) {   // build the order for the next renders of this shard
+                std::vector<unsigned> c(g.n_pixels);
+                HIP_TRY(hipMemcpyAsync(c.data(), cost, sizeof(unsigned) * g.n_pixels, hipMemcpyDeviceToHost, stream));
+                HIP_TRY(hipStreamSynchronize(stream));
+                std::vector<int> ord(g.n_pixels);
+                for (long long k = 0; k < g.n_pixels; ++k) ord[k] = (int)k;
+                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return c[a] > c[b]; });
+                HIP_TRY(hipMemcpy(d->order, ord.data(), sizeof(int) * g.n_pixels, hipMemcpyHostToDevice));
+                d->order_n = g.n_pixels;
+                d->order_key[0] = rank;
+                d->order_key[1] = world;
+                d->order_key[2] = rb;
+                d->order_valid = true;
+            }
         } else {
             // persistent wave kernel: exactly the resident blocks (occupancy query), capped by the work
             int per_cu = 0;
@@ -832,6 +929,9 @@ void rt_device_scene_release(rt_scene *s) {
         if (d->wf_buf) (void)hipFree(d->wf_buf);
         if (d->wf_count) (void)hipFree(d->wf_count);
         if (d->wf_fetch) (void)hipFree(d->wf_fetch);
+        if (d->order) (void)hipFree(d->order);
+        if (d->order_cost) (void)hipFree(d->order_cost);
+        if (d->mega_tfin) (void)hipFree(d->mega_tfin);
         if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
         for (hipStream_t &x : d->wf_stream)
             if (x) (void)hipStreamDestroy(x);

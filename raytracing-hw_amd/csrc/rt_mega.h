@@ -24,6 +24,7 @@ enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2 };
 struct MegaLane {
     long long pix;   // shard pixel (slot), -1 = none
     int s, power, nv, state;
+    unsigned long long work0;   // counting runs: traversal tests before this pixel (pixel cost)
     Rng rng;
     V3 sum;
     Ray r;
@@ -55,6 +56,7 @@ __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, con
     L.pix = p;
     L.s = 0;
     L.sum = V3{0.f, 0.f, 0.f};
+    L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
     const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
     const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
     L.rng = Rng{seed == 0 ? 1u : seed, 0u, 0.f};
@@ -65,7 +67,7 @@ __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, con
 // fold, accumulate, next sample or pixel done.
 template <bool COUNT>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
-                                           int spp, float *out, const NodeRec &root, Counters &cnt) {
+                                           int spp, float *out, unsigned *cost, const NodeRec &root, Counters &cnt) {
     AosRec P{st.rec_ab, st.rec_c, L.pix, st.D, V3{0.f, 0.f, 0.f}, 0, false};
     const Hit h = L.T.best;
     bool next = false;
@@ -83,6 +85,7 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
         out[3 * L.pix + 0] = L.sum.x;
         out[3 * L.pix + 1] = L.sum.y;
         out[3 * L.pix + 2] = L.sum.z;
+        if (COUNT && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
         L.pix = -1;
         L.state = M_IDLE;
         return;
@@ -94,10 +97,10 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
 // READY lanes this iteration (shade_now), or step the traversing lanes.
 template <bool COUNT, class Stack, class Nodes>
 __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
-                                             const WfState &st, int spp, float *out, const NodeRec &root, Stack &stk,
-                                             const Nodes &nodes, Counters &cnt) {
+                                             const WfState &st, int spp, float *out, unsigned *cost,
+                                             const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt) {
     if (shade_now) {
-        if (L.state == M_READY) mega_shade<COUNT>(L, sc, g, st, spp, out, root, cnt);
+        if (L.state == M_READY) mega_shade<COUNT>(L, sc, g, st, spp, out, cost, root, cnt);
     } else if (L.state == M_TRAV) {
         if (trav_step<COUNT>(sc, L.r, L.T, stk, nodes, cnt)) L.state = M_READY;
     }

@@ -271,7 +271,7 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
             const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
             for (int l = 0; l < 64; ++l) {
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
-                rtd::mega_iterate<true>(W[l], shade_now, sc, g, st, spp, out, root, S, nodes, cnt);
+                rtd::mega_iterate<true>(W[l], shade_now, sc, g, st, spp, out, nullptr, root, S, nodes, cnt);
             }
         }
     }

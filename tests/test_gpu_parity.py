@@ -122,3 +122,17 @@ def test_wavefront_queue_modes(gpu, monkeypatch, compact_below, groups):
     g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
     assert np.array_equal(rtref.bits(out), rtref.bits(g["sums"].reshape(-1, 3)))
     assert st["rays"] == int(g["counters"][0]) and st["aabb_tests"] == int(g["counters"][1])
+
+
+def test_reordered_pixels_same_frame(gpu):
+    """The default kernel renders the heaviest pixels first once a counting render of the
+    same shard has measured them; the frame must not change."""
+    name, w, h, s = "sponza_mini", 64, 36, 4
+    scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
+    first, _ = _sums(scene, s, count=True)          # natural order, records per-pixel cost
+    again, st = _sums(scene, s, count=True)         # heaviest-first order
+    third, _ = _sums(scene, s)
+    ref = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["sums"].reshape(-1, 3)
+    for out in (first, again, third):
+        assert np.array_equal(rtref.bits(out), rtref.bits(ref))
+    assert st["rays"] == int(rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["counters"][0])
