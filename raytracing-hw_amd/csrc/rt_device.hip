@@ -59,7 +59,6 @@ struct rt_device_scene {
     int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
     int mega_wpe = 5;                  // RT_MEGA_WPE: minimum waves per SIMD the register allocation targets
     int mega_reorder = 1;              // RT_MEGA_REORDER: heaviest-first pixel order from the last counting render
-    int mega_prio = 0;                 // RT_MEGA_PRIO: wave priority levels of this many traversal tests (0 = off)
     int mega_times = 0;                // RT_MEGA_TIMES: diagnostics, per-pixel finish-time percentiles
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
@@ -188,7 +187,6 @@ template <bool COUNT, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
                                                        int shade_min, const int *order, unsigned *cost,
-                                                       const unsigned *prio_cost, unsigned prio_unit,
                                                        unsigned long long *tfin) {
     const int lane = threadIdx.x & 63;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -215,24 +213,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                     if (p < g.n_pixels) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : p, root, cnt);
                 }
                 if ((long long)base + cm >= g.n_pixels) exhausted = true;
-                if (prio_cost) {   // waves holding the costliest pixels issue first (s_setprio)
-                    unsigned c = L.pix >= 0 ? prio_cost[L.pix] : 0u;
-                    for (int off = 32; off > 0; off >>= 1) c = max(c, (unsigned)__shfl_xor((int)c, off, 64));
-                    const unsigned lvl = c / prio_unit;
-                    if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
-                    else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-                    else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
+
             }
         }
         if (!__any(L.pix >= 0)) break;
         const int nr = __popcll(__ballot(L.state == rtd::M_READY));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
         const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
-        const long long pix_before = L.pix;
-        rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
-        if (tfin && pix_before >= 0 && L.pix < 0) tfin[pix_before] = wall_clock64();   // diagnostics
+        if (COUNT && tfin) {   // diagnostics (RT_MEGA_TIMES, counting renders only)
+            const long long pix_before = L.pix;
+            rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
+            if (pix_before >= 0 && L.pix < 0) tfin[pix_before] = wall_clock64();
+        } else {
+            rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
+        }
     }
     flush_counters<COUNT>(cnt, counters);
 }
@@ -486,6 +480,29 @@ std::vector<float> bfs_nodes(const std::vector<float> &node) {
     return out;
 }
 
+// Device texture layout: texture t's texels in 4x4 tiles, tile (tx, ty) at tile index
+// ty * ceil(w/4) + tx, texel (x & 3, y & 3) at 4 * (y & 3) + (x & 3) inside it; tex_info keeps
+// (offset in texels, width, height, channels).
+void tile_textures(const std::vector<uint32_t> &info, const std::vector<uint8_t> &texels, std::vector<uint32_t> &info_out,
+                   std::vector<uint32_t> &out) {
+    const size_t n = info.size() / 4;
+    info_out = info;
+    out.clear();
+    for (size_t t = 0; t < n; ++t) {
+        const uint32_t off = info[4 * t], w = info[4 * t + 1], h = info[4 * t + 2];
+        const uint32_t tw = (w + 3) / 4, th = (h + 3) / 4;
+        const size_t base = out.size();
+        info_out[4 * t] = (uint32_t)base;
+        out.resize(base + (size_t)tw * th * 16, 0u);
+        for (uint32_t y = 0; y < h; ++y)
+            for (uint32_t x = 0; x < w; ++x) {
+                uint32_t v;
+                std::memcpy(&v, &texels[4 * ((size_t)off + (size_t)y * w + x)], 4);
+                out[base + ((size_t)(y >> 2) * tw + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3)] = v;
+            }
+    }
+}
+
 int ensure_device_scene(rt_scene *s, int device) {
     if (s->dev && s->dev->device == device) return RT_OK;
     if (s->dev) rt_device_scene_release(s);
@@ -507,8 +524,12 @@ int ensure_device_scene(rt_scene *s, int device) {
     const size_t o_tri = append(blob, s->tri), o_attr = append(blob, s->tri_attr), o_tan = append(blob, s->tri_tan),
                  o_node = append(blob, bfs_nodes(s->node), 32), o_light = append(blob, s->light),
                  o_lnode = append(blob, s->light_node), o_mf = append(blob, s->mesh_f),
-                 o_mt = append(blob, s->mesh_tex), o_nt = append(blob, s->mesh_nt), o_ti = append(blob, s->tex_info),
-                 o_tx = append(blob, s->texels);
+                 o_mt = append(blob, s->mesh_tex), o_nt = append(blob, s->mesh_nt);
+    // textures in 4x4-texel tiles (64 B, one cache line): a bilinear 2x2 footprint usually
+    // stays in one line instead of always spanning two rows (rt_path.h tex_sample)
+    std::vector<uint32_t> tinfo, tiled;
+    tile_textures(s->tex_info, s->texels, tinfo, tiled);
+    const size_t o_ti = append(blob, tinfo), o_tx = append(blob, tiled);
     std::vector<float> lut(512);
     rtd::fill_decode_lut(lut.data());
     const size_t o_lut = append(blob, lut);
@@ -539,7 +560,6 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_WPE")) d->mega_wpe = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_REORDER")) d->mega_reorder = std::atoi(e);
-    if (const char *e = std::getenv("RT_MEGA_PRIO")) d->mega_prio = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_TIMES")) d->mega_times = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
@@ -810,7 +830,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const bool same = many && d->order && d->order_n == g.n_pixels && d->order_key[0] == rank &&
                               d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && d->mega_reorder;
             unsigned *cost = nullptr;
-            if (count && st && ((d->mega_reorder && many) || d->mega_prio > 0)) {
+            if (count && st && d->mega_reorder && many) {
                 if (d->order_cap < g.n_pixels) {
                     if (d->order) (void)hipFree(d->order);
                     if (d->order_cost) (void)hipFree(d->order_cost);
@@ -834,15 +854,11 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipStreamSynchronize(stream));
                 t_launch = 0;
             }
-            // wave priority from the same per-pixel costs (RT_MEGA_PRIO = cost unit per level, 0 = off)
-            const bool prio_ok = d->mega_prio > 0 && d->order_cost && d->order_n == g.n_pixels && d->order_key[0] == rank &&
-                                 d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && !cost;
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
                                d->mega_shade_min, same ? (const int *)d->order : nullptr, cost,
-                               prio_ok ? (const unsigned *)d->order_cost : nullptr, (unsigned)std::max(1, d->mega_prio),
                                d->mega_times ? d->mega_tfin : nullptr);
             HIP_TRY(hipGetLastError());
-            if (d->mega_times) {   // print finish-time percentiles (ms after the first finish) to stderr
+            if (d->mega_times && count) {   // print finish-time percentiles (ms after the first finish) to stderr
                 std::vector<unsigned long long> t(g.n_pixels);
                 HIP_TRY(hipMemcpyAsync(t.data(), d->mega_tfin, sizeof(unsigned long long) * g.n_pixels,
                                        hipMemcpyDeviceToHost, stream));

@@ -382,7 +382,13 @@ __device__ __forceinline__ V4 tex_sample(const DevScene &sc, int tex, V2 p, bool
 #pragma unroll
         for (int ddx = 0; ddx < 2; ++ddx) {
             const int x = (px + ddx) % W, y = (py + ddy) % H;
-            texel[ddx * 2 + ddy] = sc.texels[ti.x + (uint32_t)(y * W + x)];
+#ifdef __HIPCC__
+            // device copy: 4x4-texel tiles (rt_device.hip tile_textures)
+            const uint32_t idx = (uint32_t)(((y >> 2) * ((W + 3) >> 2) + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3));
+#else
+            const uint32_t idx = (uint32_t)(y * W + x);   // host view: row-major
+#endif
+            texel[ddx * 2 + ddy] = sc.texels[ti.x + idx];
         }
     float res[4];
 #pragma unroll
