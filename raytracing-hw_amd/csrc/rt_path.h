@@ -489,11 +489,15 @@ __device__ __forceinline__ float smith(float alpha, V3 N, V3 V, V3 L) {
 // matrix.h:66-86 multiplyVector with matrix4d: float accumulators, each add in double.
 __device__ __forceinline__ V3 mul_vector_d(const double *m, V3 t) {
     const float tv[4] = {t.x, t.y, t.z, 0.f};
-    float res[4] = {0.f, 0.f, 0.f, 0.f};
+    float res[3] = {0.f, 0.f, 0.f};
+    // column by column (same per-component addition order j = 0..3); not unrolled over j so
+    // that only one column of doubles is live at a time (register pressure in shading)
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j) {
+        const double tj = (double)tv[j];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) res[i] = (float)((double)res[i] + m[4 * j + i] * (double)tv[j]);
+        for (int i = 0; i < 3; ++i) res[i] = (float)((double)res[i] + m[4 * j + i] * tj);
+    }
     return V3{res[0], res[1], res[2]};
 }
 
