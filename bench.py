@@ -5,7 +5,8 @@
 
 A step = one full frame of the workload: every pixel of the 1920x1080 frame traced at
 256 spp, depth 6, split into interleaved 8-row blocks over the N ranks (one MI355X each),
-followed by the RCCL all-gather of the float framebuffer.  Rank 0 prints one JSON line.
+finished to the 8-bit frame on each GPU (rt_tonemap_u8_device, scene.cpp:54-64) and
+all-gathered over RCCL (6.2 MB).  Rank 0 prints one JSON line.
 
 value    = scene closest-hit queries (rays, counted in-kernel during warmup; the count is
            deterministic per frame) of all ranks x K / max-over-ranks wall time of the K steps
@@ -140,13 +141,16 @@ def main():
     rtdist = importlib.import_module("raytracing_hw_amd.dist")
     max_rows = rtdist.max_shard_rows(H, world, args.row_block)
     out = torch.zeros(max_rows * W * 3, dtype=torch.float32, device="cuda")
-    frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(max_rows * W * 3, dtype=torch.uint8, device="cuda")
+    frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(count=False):
+        # render the shard, finish it to 8 bits on the GPU (scene.cpp:54-64), gather the frame
         st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
                                  count=count, kernel=args.kernel, stats=True, kernel_times=not count)
-        rtdist.gather_frame(out, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
+        rt.tonemap_device(out.data_ptr(), W, max_rows, S, rgb.data_ptr(), stream)
+        rtdist.gather_frame(rgb, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
         return st
 
     # warmup; the first one counts rays / tests (deterministic per frame, so valid for every step)

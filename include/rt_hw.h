@@ -10,6 +10,7 @@
  *                        <- Scene::render sample loop   src/core/scene.cpp:17-52
  *                           (per-pixel float RGB sums = sample_canvas, scene.cpp:20,42)
  *   rt_tonemap_u8        <- Scene::render frame finish  src/core/scene.cpp:54-64
+ *   rt_tonemap_u8_device <- the same finish on the GPU   src/core/scene.cpp:54-64
  *   rt_write_ppm         <- Canvas::write_to            src/render/canvas.h:76-89
  *   rt_last_error        <- the reference's std::runtime_error messages (23 throw sites);
  *                           the host wrappers re-throw them (drop-in failure behaviour).
@@ -143,6 +144,10 @@ int rt_intersect_rays(rt_scene *scene, int64_t n, const float *org, const float 
 /* --- frame finish / output (host) ---------------------------------------------------- */
 /* mean -> ACES -> powf(1/2.2) -> roundf(clamp(v*255)) per scene.cpp:54-64, vector.h:222-233, :400-407 */
 int rt_tonemap_u8(const float *sum, int32_t width, int32_t height, int32_t spp, uint8_t *rgb_out);
+/* The same finish on the device (current HIP device, asynchronous on `stream`): d_sum and
+ * d_rgb are device pointers; bit-identical to rt_tonemap_u8 (the gamma quantizer is glibc
+ * powf's, as exact thresholds). */
+int rt_tonemap_u8_device(const float *d_sum, int32_t width, int32_t height, int32_t spp, uint8_t *d_rgb, void *stream);
 /* "P6\n{W} {H}\n255\n" + raw RGB (canvas.h:76-89) */
 int rt_write_ppm(const char *path, const uint8_t *rgb, int32_t width, int32_t height);
 

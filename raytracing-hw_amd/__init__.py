@@ -80,6 +80,8 @@ ABI = {
     "rt_intersect_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_f, _c_f, _c_f,
                                          ctypes.POINTER(ctypes.c_int64)]),
     "rt_tonemap_u8": (ctypes.c_int, [_c_f, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _c_b]),
+    "rt_tonemap_u8_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_void_p, ctypes.c_void_p]),
     "rt_write_ppm": (ctypes.c_int, [ctypes.c_char_p, _c_b, ctypes.c_int32, ctypes.c_int32]),
     "rt_last_error": (ctypes.c_char_p, []),
     "rt_abi_version": (ctypes.c_int32, []),
@@ -278,6 +280,12 @@ def tonemap(sums, spp):
     rgb = np.zeros((h, w, 3), np.uint8)
     _check(lib().rt_tonemap_u8(sums.ctypes.data_as(_c_f), w, h, spp, rgb.ctypes.data_as(_c_b)))
     return rgb
+
+
+def tonemap_device(d_sum_ptr, width, height, spp, d_rgb_ptr, stream_ptr=None):
+    """rt_tonemap_u8_device: the frame finish on the GPU (device pointers, e.g. torch tensors)."""
+    _check(lib().rt_tonemap_u8_device(ctypes.c_void_p(d_sum_ptr), width, height, spp, ctypes.c_void_p(d_rgb_ptr),
+                                      ctypes.c_void_p(stream_ptr or 0)))
 
 
 def write_ppm(filename, rgb):

@@ -21,6 +21,7 @@
 #include "rt_wave.h"
 #include "rt_wavefront.h"
 #include "rt_mega.h"
+#include "rt_quant_lut.h"
 #include "rt_scene.h"
 
 using rtd::Counters;
@@ -178,6 +179,35 @@ __global__ void __launch_bounds__(256) rt_wave_kernel(DevScene sc, ShardGeom g, 
         if (L.state == rtd::L_SHADE) rtd::lane_shade<COUNT>(L, sc, spp, out, cnt);
     }
     flush_counters<COUNT>(cnt, counters);
+}
+
+// ------------------------------------------------------------------------ frame finish
+// Scene::render's last loop (scene.cpp:54-64) on the device: mean, ACES (vector.h:400-407,
+// same operation order as rt_tonemap_u8), saturate, then powf(v, 1/2.2) + round(clamp(*255))
+// as the exact threshold count of rt_quant_lut.h (glibc powf quantizer, checked monotonic
+// over every float in [0, 1] by tools/libm_check.cpp).  NaN gives 0, as on the host.
+__constant__ uint32_t k_quant_thr[256];
+__global__ void __launch_bounds__(256) rt_finish_kernel(const float *sum, long long n, float normalizer,
+                                                         uint8_t *rgb) {
+    __shared__ float thr[256];
+    thr[threadIdx.x] = __uint_as_float(k_quant_thr[threadIdx.x]);
+    __syncthreads();
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        float x = sum[i];
+        x *= normalizer;
+        const float num = x * (x * 2.51f + 0.03f);
+        const float den = x * (x * 2.43f + 0.59f) + 0.14f;
+        const float v = rtv::smax(rtv::smin(num / den, 1.f), 0.f);
+        int q = 0;
+        if (!isnan(v)) {   // #{k in 1..255 : thr[k] <= v}, binary search (thr is non-decreasing)
+            int lo = 0;    // invariant: thr[lo] <= v (thr[0] = 0 <= v for v >= 0)
+#pragma unroll
+            for (int step = 128; step > 0; step >>= 1)
+                if (lo + step <= 255 && thr[lo + step] <= v) lo += step;
+            q = lo;
+        }
+        rgb[i] = (uint8_t)q;
+    }
 }
 
 // ------------------------------------------------------------------------ lane-resident (kernel 4)
@@ -967,6 +997,25 @@ int rt_scene_upload(rt_scene *s, int32_t device) {
 
 int rt_render_device(rt_scene *s, const rt_params *p, float *d_out, void *stream, rt_stats *st) {
     return launch(s, p, d_out, (hipStream_t)stream, st);
+}
+
+int rt_tonemap_u8_device(const float *d_sum, int32_t width, int32_t height, int32_t spp, uint8_t *d_rgb, void *stream) {
+    if (!d_sum || !d_rgb || width <= 0 || height <= 0 || spp <= 0)
+        return rt_fail(RT_ERR_ARG, "rt_tonemap_u8_device: bad argument");
+    static bool uploaded[64] = {false};
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return rt_fail(RT_ERR_DEVICE, "rt_tonemap_u8_device: device id");
+    if (!uploaded[dev]) {
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(k_quant_thr), rtm::kQuantThr, sizeof rtm::kQuantThr));
+        uploaded[dev] = true;
+    }
+    const long long n = (long long)width * height * 3;
+    const unsigned blocks = (unsigned)std::min<long long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(rt_finish_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_sum, n,
+                       1.f / (float)spp, d_rgb);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
 }
 
 int rt_render(rt_scene *s, const rt_params *p, float *out, rt_stats *st) {

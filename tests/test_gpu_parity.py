@@ -17,6 +17,11 @@ CASES = [("cornell", 64, 64, 8), ("cornell", 33, 17, 3), ("cornell_blob", 48, 48
 
 @pytest.fixture(scope="module")
 def gpu(rt):
+    # torch first: it must initialise the HIP runtime it shares with librt_hw_amd.so
+    # (torch cannot initialise after the library has)
+    import torch
+    if torch.cuda.is_available():
+        torch.zeros(1, device="cuda")
     if rt.device_count() < 1:
         pytest.fail("no HIP device visible: the GPU tests must run on the MI355X box")
     return rt
@@ -136,3 +141,28 @@ def test_reordered_pixels_same_frame(gpu):
     for out in (first, again, third):
         assert np.array_equal(rtref.bits(out), rtref.bits(ref))
     assert st["rays"] == int(rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["counters"][0])
+
+
+def test_device_finish_matches_reference(gpu):
+    """rt_tonemap_u8_device (scene.cpp:54-64 on the GPU) against the reference's own 8-bit
+    finish of the golden sums (NaN, inf, negative, saturating values included) and against
+    the host rt_tonemap_u8 on a wide random range."""
+    import torch
+    g = rtref.golden("finish_37x23x16.rtd")
+    spp = int(g["spp"][0])
+    want = open(rtref.os.path.join(rtref.GOLD, "finish_37x23x16.ppm"), "rb").read()[len(b"P6\n37 23\n255\n"):]
+    d_sum = torch.from_numpy(np.ascontiguousarray(g["sums"], np.float32)).cuda()
+    d_rgb = torch.zeros(d_sum.numel(), dtype=torch.uint8, device="cuda")
+    gpu.tonemap_device(d_sum.data_ptr(), 37, 23, spp, d_rgb.data_ptr())
+    torch.cuda.synchronize()
+    assert d_rgb.cpu().numpy().tobytes() == want
+    rng = np.random.default_rng(7)
+    sums = (rng.standard_normal((300, 200, 3)) * np.exp(rng.uniform(-20, 8, (300, 200, 3)))).astype(np.float32)
+    sums.reshape(-1)[::997] = np.nan
+    sums.reshape(-1)[::991] = np.inf
+    host = gpu.tonemap(sums, 16)
+    d_sum = torch.from_numpy(sums).cuda()
+    d_rgb = torch.zeros(sums.size, dtype=torch.uint8, device="cuda")
+    gpu.tonemap_device(d_sum.data_ptr(), 200, 300, 16, d_rgb.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(d_rgb.cpu().numpy().reshape(300, 200, 3), host)

@@ -33,3 +33,12 @@ def test_srgb_lut_is_glibc_powf(checker):
     r = subprocess.run([checker, "lut"], capture_output=True, text=True, check=True)
     committed = open(os.path.join(ROOT, "raytracing-hw_amd", "csrc", "rt_srgb_lut.h")).read()
     assert r.stdout == committed
+
+
+@pytest.mark.slow
+def test_gamma_quantizer_thresholds(checker):
+    """rt_quant_lut.h: the 8-bit gamma step's thresholds from glibc powf (the generator
+    also checks the quantizer is monotonic over every float in [0, 1])."""
+    r = subprocess.run([checker, "quant"], capture_output=True, text=True, check=True, timeout=600)
+    committed = open(os.path.join(ROOT, "raytracing-hw_amd", "csrc", "rt_quant_lut.h")).read()
+    assert r.stdout == committed
