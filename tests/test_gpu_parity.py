@@ -151,7 +151,7 @@ def test_device_finish_matches_reference(gpu):
     g = rtref.golden("finish_37x23x16.rtd")
     spp = int(g["spp"][0])
     want = open(rtref.os.path.join(rtref.GOLD, "finish_37x23x16.ppm"), "rb").read()[len(b"P6\n37 23\n255\n"):]
-    d_sum = torch.from_numpy(np.ascontiguousarray(g["sums"], np.float32)).cuda()
+    d_sum = torch.from_numpy(np.array(g["sums"], np.float32, copy=True)).cuda()
     d_rgb = torch.zeros(d_sum.numel(), dtype=torch.uint8, device="cuda")
     gpu.tonemap_device(d_sum.data_ptr(), 37, 23, spp, d_rgb.data_ptr())
     torch.cuda.synchronize()
