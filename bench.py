@@ -93,6 +93,21 @@ def cpu_baseline(scene_path, width, height, spp, rows, threads):
             "sample": sample + " (oracle/rt_oracle.cpp restatement)", "seconds": secs}
 
 
+def pmc_traffic(fetch_csv, write_csv, kernel_prefix):
+    """HBM-side bytes per launch of `kernel_prefix` from rocprofv3 PMC summaries
+    (tools/profile.sh, separate --pmc passes of the same command): FETCH_SIZE doubled (the
+    gfx950 correction of MI355X_MICROARCH.md, HBM section; FETCH_SIZE counts half of the
+    bytes of 16-B-per-lane reads) plus WRITE_SIZE, both KiB per dispatch."""
+    import csv
+    def mean(path, counter):
+        for row in csv.reader(open(path)):
+            if row and row[0].startswith(kernel_prefix) and row[1] == counter:
+                return float(row[4]) * 1024.0
+        return None
+    f, w = mean(fetch_csv, "FETCH_SIZE"), mean(write_csv, "WRITE_SIZE")
+    return None if f is None or w is None else 2.0 * f + w
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +123,10 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the frame in the CPU baseline sample")
     ap.add_argument("--cpu-spp", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-from", default="auto",
+                    help="PMC summaries for roofline.traffic: a path prefix P (P_fetch*.csv / P_write*.csv from "
+                         "tools/profile.sh of this same command), 'auto' (the committed profiles/ pair when the "
+                         "workload is the default one) or 'none'")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,6 +224,19 @@ def main():
             bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
             kname = ["rt_mega_kernel", "rt_pixels_kernel", "rt_persistent_kernel", "rt_wave_kernel"][args.kernel]
         achieved = bytes_launch / avg_s / 1e9
+        traffic, traffic_src = None, None
+        if args.traffic_from != "none":
+            prefix = args.traffic_from
+            default_cfg = (args.scene, W, H, S, args.kernel) == ("sponza", 1920, 1080, 256, 0)
+            if prefix == "auto":
+                prefix = os.path.join(ROOT, "profiles", "r01_final") if default_cfg else None
+            if prefix:
+                fc, wc = prefix + "_fetch_1080p256.csv", prefix + "_write_1080p256.csv"
+                if os.path.exists(fc) and os.path.exists(wc):
+                    t = pmc_traffic(fc, wc, "void " + kname + "<false")
+                    if t is not None:
+                        traffic = t / launches
+                        traffic_src = os.path.relpath(fc, ROOT) + " + " + os.path.relpath(wc, ROOT)
         line = {
             "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -226,7 +258,9 @@ def main():
                        "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else int(traffic),
+                         "traffic_source": traffic_src,
                          "kernel": kname, "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
                          "launches_per_frame": launches,
                          "path_frame_bytes": int(bytes_frame), "path_frame_ms": round(frame_s * 1e3, 3),
