@@ -1,9 +1,10 @@
-// rt_mega.h — lane-resident path tracer for small shards (kernel 4).
+// rt_mega.h — lane-resident path tracer (kernel 0, the default).
 //
 // The wavefront (rt_wavefront.h) advances every path one bounce per launch pair, so each
 // iteration costs as much as the slowest ray of the whole frame; with few paths per GPU
 // (a 1080p frame split over 8 GPUs leaves ~260 k pixels each, about one per lane) the
-// frame time becomes the sum over ~1500 iterations of that maximum.  Here every lane owns
+// frame time becomes the sum over ~1500 iterations of that maximum.  The wavefront is
+// kernel 4.  Here every lane owns
 // one pixel at a time and runs its whole sample loop (scene.cpp:34-42) itself, so a path
 // only ever waits for its own rays:
 //   * traversal advances every traversing lane of a wave by one unit per iteration
