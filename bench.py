@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--kernel", type=int, default=0, help="0 lane-resident (default), 1 one lane per pixel, "
                     "2 persistent per pixel, 3 wave megakernel, 4 wavefront")
     ap.add_argument("--row-block", type=int, default=8)
-    ap.add_argument("--cpu-rows", type=int, default=540, help="rows of the frame in the CPU baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=1080, help="rows of the frame in the CPU baseline sample")
     ap.add_argument("--cpu-spp", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-from", default="auto",

@@ -60,6 +60,8 @@ struct rt_device_scene {
     int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
     int mega_wpe = 5;                  // RT_MEGA_WPE: minimum waves per SIMD the register allocation targets
     int mega_reorder = 1;              // RT_MEGA_REORDER: heaviest-first pixel order from the last counting render
+    int mega_occ = 0;                  // RT_MEGA_OCC: resident blocks per CU for kernel 0 (0 = occupancy limit)
+    int mega_order_min = 3;            // RT_MEGA_ORDER_MIN: reorder only with >= this many pixels per lane
     int mega_times = 0;                // RT_MEGA_TIMES: diagnostics, per-pixel finish-time percentiles
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
@@ -213,6 +215,13 @@ __global__ void __launch_bounds__(256) rt_finish_kernel(const float *sum, long l
 // ------------------------------------------------------------------------ lane-resident (kernel 4)
 // rt_mega.h: every lane runs whole pixels; traversal one unit per iteration, shading batched
 // per wave (READY lanes wait for `shade_min` of them or for no lane left traversing).
+#ifdef RT_MEGA_PROF
+// Diagnostics build (make EXTRA=-DRT_MEGA_PROF): per-wave clock64() split of the main loop.
+// [0] shade-iteration cycles [1] traversal-iteration cycles [2] pixel-assign cycles
+// [3] shade iterations [4] traversal iterations [5] sum of ready lanes over shade iterations
+// [6] sum of traversing lanes over traversal iterations [7] waves
+__device__ unsigned long long g_mega_prof[8];
+#endif
 template <bool COUNT, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
@@ -228,6 +237,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     L.pix = -1;
     L.state = rtd::M_IDLE;
     bool exhausted = false;
+#ifdef RT_MEGA_PROF
+    unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
+    long long tp = clock64();
+#endif
     for (;;) {
         if (!exhausted) {   // lanes without a pixel take the next ones (one atomic per wave)
             const bool need = L.pix < 0;
@@ -250,6 +263,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         const int nr = __popcll(__ballot(L.state == rtd::M_READY));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
         const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
+#ifdef RT_MEGA_PROF
+        {
+            const long long t1 = clock64();
+            pf[2] += (unsigned long long)(t1 - tp);
+            tp = t1;
+            pf[shade_now ? 3 : 4] += 1;
+            pf[shade_now ? 5 : 6] += (unsigned long long)(shade_now ? nr : nt);
+        }
+#endif
         if (COUNT && tfin) {   // diagnostics (RT_MEGA_TIMES, counting renders only)
             const long long pix_before = L.pix;
             rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
@@ -257,7 +279,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         } else {
             rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
         }
+#ifdef RT_MEGA_PROF
+        {
+            const long long t1 = clock64();
+            pf[shade_now ? 0 : 1] += (unsigned long long)(t1 - tp);
+            tp = t1;
+        }
+#endif
     }
+#ifdef RT_MEGA_PROF
+    if (lane == 0) {
+        for (int k = 0; k < 7; ++k) atomicAdd(&g_mega_prof[k], pf[k]);
+        atomicAdd(&g_mega_prof[7], 1ull);
+    }
+#endif
     flush_counters<COUNT>(cnt, counters);
 }
 
@@ -590,6 +625,8 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_WPE")) d->mega_wpe = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_REORDER")) d->mega_reorder = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_OCC")) d->mega_occ = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("RT_MEGA_ORDER_MIN")) d->mega_order_min = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_TIMES")) d->mega_times = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
@@ -849,6 +886,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             int per_cu = 0;
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk, 256, 0));
             if (per_cu < 1) per_cu = 1;
+            if (d->mega_occ > 0) per_cu = std::min(per_cu, d->mega_occ);
             const long long need = (g.n_pixels + 255) / 256;
             unsigned blocks = (unsigned)std::min<long long>(need, (long long)d->cu_count * per_cu);
             if (blocks == 0) blocks = 1;
@@ -856,7 +894,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             // this shard (the frame's tail is then made of cheap pixels); natural order otherwise
             // (only with >= 3 pixels per lane: with fewer, every lane starts at once and sorting
             // only clusters the heavy pixels on the same SIMDs — measured slower at 4 and 8 GPUs)
-            const bool many = g.n_pixels >= 3LL * blocks * 256;
+            const bool many = g.n_pixels >= (long long)d->mega_order_min * blocks * 256;
             const bool same = many && d->order && d->order_n == g.n_pixels && d->order_key[0] == rank &&
                               d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && d->mega_reorder;
             unsigned *cost = nullptr;
@@ -884,10 +922,31 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipStreamSynchronize(stream));
                 t_launch = 0;
             }
+#ifdef RT_MEGA_PROF
+            {
+                const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
+            }
+#endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
                                d->mega_shade_min, same ? (const int *)d->order : nullptr, cost,
                                d->mega_times ? d->mega_tfin : nullptr);
             HIP_TRY(hipGetLastError());
+#ifdef RT_MEGA_PROF
+            {
+                unsigned long long pf[8];
+                HIP_TRY(hipMemcpyFromSymbolAsync(pf, HIP_SYMBOL(g_mega_prof), sizeof pf, 0, hipMemcpyDeviceToHost, stream));
+                HIP_TRY(hipStreamSynchronize(stream));
+                const double tot = (double)(pf[0] + pf[1] + pf[2]);
+                std::fprintf(stderr,
+                             "[mega prof] count=%d waves=%llu cycles/wave=%.3g shade=%.3f trav=%.3f assign=%.3f "
+                             "shade_iters/wave=%.0f trav_iters/wave=%.0f ready/shade=%.1f trav_lanes/iter=%.1f "
+                             "cyc/shade_iter=%.0f cyc/trav_iter=%.0f\n",
+                             (int)count, pf[7], tot / pf[7], pf[0] / tot, pf[1] / tot, pf[2] / tot,
+                             (double)pf[3] / pf[7], (double)pf[4] / pf[7], (double)pf[5] / pf[3],
+                             (double)pf[6] / pf[4], (double)pf[0] / pf[3], (double)pf[1] / pf[4]);
+            }
+#endif
             if (d->mega_times && count) {   // print finish-time percentiles (ms after the first finish) to stderr
                 std::vector<unsigned long long> t(g.n_pixels);
                 HIP_TRY(hipMemcpyAsync(t.data(), d->mega_tfin, sizeof(unsigned long long) * g.n_pixels,

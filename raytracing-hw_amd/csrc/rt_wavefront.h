@@ -197,6 +197,11 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
     q[kQRec * (size_t)p] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
 }
 
+// trav_step issues the node-pair and triangle reads together (compile-time A/B knob).
+#ifndef RT_HOIST_LOADS
+#define RT_HOIST_LOADS 1
+#endif
+
 // Resumable traversal state of one ray.
 enum TravPhase : int { TP_NODE = 0, TP_LEAF = 1, TP_POP = 2 };
 struct TravState {
@@ -205,7 +210,6 @@ struct TravState {
     float acc;       // best t inside the subtree being traversed (the reference's local best)
     int sp;
     int phase;
-    uint32_t dpos;   // bit i: dir[i] > 0 (near-child choice, bvh.cpp:196-203)
     Hit best;        // global winner so far (strict <, first of equal t wins)
 };
 
@@ -246,7 +250,6 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
     T.best.u = T.best.v = 0.f;
     T.sp = 0;
     T.acc = 1e9f;
-    T.dpos = bits & 7u;
     trav_enter(T, root_a, root_b);
     return (bits & 8u) == 0;
 }
@@ -258,13 +261,30 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
 template <bool COUNT, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, const Nodes &nodes,
                                           Counters &cnt) {
-    if (T.phase == TP_NODE) {
+    const bool at_node = T.phase == TP_NODE, at_leaf = T.phase == TP_LEAF;
+    NodeRec L, R;
+    V3 v0, U, V;
+#if RT_HOIST_LOADS
+    // Both memory reads of the step issue before either test: a wave whose lanes are split
+    // between node and leaf steps waits for one round trip per iteration, not two.  Lanes in
+    // the other phase read a fixed, cached address (pair 0 / triangle 0) and ignore it.
+    nodes.load_pair(at_node ? T.a : 0u, L, R);
+    load_tri(sc.tri, at_leaf ? (int)T.k : 0, v0, U, V);
+#ifdef __HIPCC__
+    // (pin the loads here: otherwise the compiler sinks each into its own branch again)
+    asm volatile("" ::"v"(L.mn[0]), "v"(L.mx[1]), "v"(R.mn[0]), "v"(R.mx[1]), "v"(v0.x), "v"(U.y), "v"(V.z));
+#endif
+#endif
+    if (at_node) {
         const uint32_t a = T.a, b = T.b;
         RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, T.a = 0);
-        NodeRec L, R;
+#if !RT_HOIST_LOADS
         nodes.load_pair(a, L, R);
+#endif
         if (COUNT) cnt.aabb += 2;
-        const bool lf = (T.dpos >> b) & 1u;   // dir[split axis] > 0: left child first
+        // dir[split axis] > 0: left child first (sign bits recomputed: cheaper than a register)
+        const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
+        const bool lf = (dpos >> b) & 1u;
         NodeRec N, F;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -288,11 +308,12 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
         const bool far_only = !hn && hf && !(ef > 1e9f);
         if (hn || far_only) trav_enter(T, hn ? N.a : F.a, hn ? N.b : F.b);
         else T.phase = TP_POP;
-    } else if (T.phase == TP_LEAF) {
+    } else if (at_leaf) {
         const uint32_t k = T.k;
         RT_CHECK(k < (uint32_t)sc.n_tris, 12, k, T.k = 0);
-        V3 v0, U, V;
+#if !RT_HOIST_LOADS
         load_tri(sc.tri, (int)k, v0, U, V);
+#endif
         TriHit h;
         if (COUNT) cnt.tri++;
         if (tri_hit_bl(v0, U, V, r, h)) {
