@@ -221,6 +221,7 @@ __global__ void __launch_bounds__(256) rt_finish_kernel(const float *sum, long l
 // [3] shade iterations [4] traversal iterations [5] sum of ready lanes over shade iterations
 // [6] sum of traversing lanes over traversal iterations [7] waves
 __device__ unsigned long long g_mega_prof[8];
+__device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT_PROF_SEG)
 #endif
 template <bool COUNT, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
@@ -239,6 +240,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     bool exhausted = false;
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
+    __syncthreads();
     long long tp = clock64();
 #endif
     for (;;) {
@@ -292,6 +295,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         for (int k = 0; k < 7; ++k) atomicAdd(&g_mega_prof[k], pf[k]);
         atomicAdd(&g_mega_prof[7], 1ull);
     }
+    __syncthreads();
+    if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
 #endif
     flush_counters<COUNT>(cnt, counters);
 }
@@ -926,6 +931,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             {
                 const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
@@ -945,6 +951,13 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                              (int)count, pf[7], tot / pf[7], pf[0] / tot, pf[1] / tot, pf[2] / tot,
                              (double)pf[3] / pf[7], (double)pf[4] / pf[7], (double)pf[5] / pf[3],
                              (double)pf[6] / pf[4], (double)pf[0] / pf[3], (double)pf[1] / pf[4]);
+                unsigned long long sg[8];
+                HIP_TRY(hipMemcpyFromSymbolAsync(sg, HIP_SYMBOL(g_mega_seg), sizeof sg, 0, hipMemcpyDeviceToHost, stream));
+                HIP_TRY(hipStreamSynchronize(stream));
+                std::fprintf(stderr, "[mega prof] shade segments, cycles per shade iteration: mesh+emission=%.0f "
+                             "normal=%.0f mr=%.0f sample=%.0f pdf=%.0f base+brdf=%.0f\n",
+                             (double)sg[0] / pf[3], (double)sg[1] / pf[3], (double)sg[2] / pf[3],
+                             (double)sg[3] / pf[3], (double)sg[4] / pf[3], (double)sg[5] / pf[3]);
             }
 #endif
             if (d->mega_times && count) {   // print finish-time percentiles (ms after the first finish) to stderr

@@ -46,6 +46,23 @@ __device__ unsigned long long rt_debug_word;
 #define RT_CHECK(cond, code, val, fix) do { } while (0)
 #endif
 
+// Diagnostics build (RT_MEGA_PROF): per-block clock64() sums of shading segments, added by
+// the first active lane of the shading wave (rt_device.hip zeroes and flushes them).
+#if defined(RT_MEGA_PROF) && defined(__HIPCC__)
+__shared__ unsigned long long rt_prof_lds[8];
+#define RT_PROF_BEGIN long long rt_pt_ = clock64();
+#define RT_PROF_SEG(k)                                                                                   \
+    do {                                                                                                 \
+        const long long t1_ = clock64();                                                                 \
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)                     \
+            atomicAdd(&rt_prof_lds[k], (unsigned long long)(t1_ - rt_pt_));                              \
+        rt_pt_ = t1_;                                                                                    \
+    } while (0)
+#else
+#define RT_PROF_BEGIN
+#define RT_PROF_SEG(k) do { } while (0)
+#endif
+
 namespace rtd {
 
 using rtv::V2;
@@ -597,6 +614,7 @@ struct AosRec {
 // pdf <= 0 or NaN).
 template <bool COUNT, class Rec>
 __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
+    RT_PROF_BEGIN
     if (COUNT) cnt.hits++;
     int id = hit.prim;
     RT_CHECK(id >= 0 && id < sc.n_tris, 1, id, id = 0);
@@ -618,6 +636,7 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     V3 emission{mf[3], mf[4], mf[5]};
     if (mt[3] >= 0) emission = rtv::mulv(rtv::reduce(tex_sample(sc, mt[3], tc, true)), emission);
     P.set_e(nv, emission);
+    RT_PROF_SEG(0);
     // Primitive::get_shading_normal (primitive.cpp:86-105)
     V3 n0{a0.x, a0.y, a0.z}, n1{a0.w, a1.x, a1.y}, n2{a1.z, a1.w, a2.x};
     V3 lz = rtv::normal(rtv::add(rtv::add(rtv::mul(n0, w), rtv::mul(n1, u)), rtv::mul(n2, v)));
@@ -633,6 +652,7 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
         N = rtv::normal(rtv::add(rtv::add(rtv::mul(lx, ln.x), rtv::mul(ly, ln.y)), rtv::mul(lz, ln.z)));
     }
     if (inside) N = rtv::neg(N);
+    RT_PROF_SEG(1);
     // Primitive::get_metallic_roughness (primitive.cpp:131-140)
     float r2 = mf[7], metallic = mf[6];
     if (mt[2] >= 0) {
@@ -644,13 +664,16 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     r2 = rtv::smax(kRoughness2Limit, r2);
     const V3 pos = rtv::add(r.o, rtv::mul(r.d, hit.t));
     const V3 eye = rtv::neg(r.d);
+    RT_PROF_SEG(2);
     const V3 dir = scene_sample(sc, pos, N, eye, r2, rng);
+    RT_PROF_SEG(3);
     nv++;
     if (rtv::dot(dir, N) <= 0.f) {
         if (rtv::dot(dir, ngeo) <= 0.f) return false;
         N = ngeo;
     }
     const float pdf = scene_pdf<COUNT>(sc, pos, N, eye, r2, dir, cnt);
+    RT_PROF_SEG(4);
     if (pdf <= 0.f || isnan(pdf)) return false;
     // BRDF of this vertex (scene.cpp:134-154): used only if the child ray hits
     const float coeff = 1 / pdf;
@@ -669,6 +692,7 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     P.set_brdf(nv - 1, rtv::add(rtv::mul(dielectric, 1 - metallic), rtv::mul(metal, metallic)), coeff,
                rtv::dot(dir, N), mf[8]);
     r = make_ray(rtv::add(pos, rtv::mul(dir, kStep)), dir);
+    RT_PROF_SEG(5);
     return true;
 }
 
