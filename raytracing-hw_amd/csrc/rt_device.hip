@@ -224,11 +224,17 @@ __device__ unsigned long long g_mega_prof[8];
 __device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT_PROF_SEG)
 #endif
 template <bool COUNT, int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc, ShardGeom g, rtd::WfState st, int spp, float *out,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
                                                        int shade_min, const int *order, unsigned *cost,
                                                        unsigned long long *tfin) {
     const int lane = threadIdx.x & 63;
+    // texel-decode LUT in LDS: the shading's lane-dependent lookups become ds_reads
+    __shared__ float lut[512];
+    for (int k = threadIdx.x; k < 512; k += blockDim.x) lut[k] = sc_in.lut[k];
+    __syncthreads();
+    DevScene sc = sc_in;
+    sc.lut = lut;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 spill[rtd::kStack - rtd::kLdsStack];
     rtd::LdsStack S{spill};

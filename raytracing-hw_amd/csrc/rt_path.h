@@ -384,8 +384,7 @@ __device__ float light_pdf(const DevScene &sc, V3 point, V3 direction, Counters 
 
 // ------------------------------------------------------------------------ textures
 // Texture::interpolate_sample (primitive.h:182-215); RGBA8, four channels always.
-__device__ __forceinline__ V4 tex_sample(const DevScene &sc, int tex, V2 p, bool srgb) {
-    const uint4 ti = sc.tex_info[tex];
+__device__ __forceinline__ V4 tex_sample_ti(const DevScene &sc, const uint4 ti, V2 p, bool srgb) {
     const int W = (int)ti.y, H = (int)ti.z;
     p.x -= floorf(p.x);
     p.y -= floorf(p.y);
@@ -419,6 +418,9 @@ __device__ __forceinline__ V4 tex_sample(const DevScene &sc, int tex, V2 p, bool
         res[c] = v[0] * (1 - dx) * (1 - dy) + v[1] * (1 - dx) * dy + v[2] * dx * (1 - dy) + v[3] * dx * dy;
     }
     return V4{res[0], res[1], res[2], res[3]};
+}
+__device__ __forceinline__ V4 tex_sample(const DevScene &sc, int tex, V2 p, bool srgb) {
+    return tex_sample_ti(sc, sc.tex_info[tex], p, srgb);
 }
 
 // ------------------------------------------------------------------------ sampling
@@ -630,24 +632,32 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     RT_CHECK(mesh >= 0 && mesh < sc.n_meshes, 3, mesh, mesh = 0);
     const float *mf = sc.mesh_f + 12 * mesh;
     const int *mt = sc.mesh_tex + 4 * mesh;
+    // texture descriptors of the emission, normal and metallic-roughness slots, read together
+    // (one round trip, not one per texture on the way)
+    const int mt_e = mt[3], mt_n = mt[1], mt_mr = mt[2];
+    const uint4 ti_e = sc.tex_info[mt_e >= 0 ? mt_e : 0], ti_n = sc.tex_info[mt_n >= 0 ? mt_n : 0],
+                ti_mr = sc.tex_info[mt_mr >= 0 ? mt_mr : 0];
+#ifdef __HIPCC__
+    asm volatile("" ::"v"(ti_e.x), "v"(ti_n.x), "v"(ti_mr.x));   // (keep the reads here, not sunk into the branches)
+#endif
     const float w = 1 - u - v;
     const V2 tc{w * a2.y + u * a2.w + v * a3.y, w * a2.z + u * a3.x + v * a3.z};
     // Primitive::get_emission (primitive.cpp:121-129)
     V3 emission{mf[3], mf[4], mf[5]};
-    if (mt[3] >= 0) emission = rtv::mulv(rtv::reduce(tex_sample(sc, mt[3], tc, true)), emission);
+    if (mt_e >= 0) emission = rtv::mulv(rtv::reduce(tex_sample_ti(sc, ti_e, tc, true)), emission);
     P.set_e(nv, emission);
     RT_PROF_SEG(0);
     // Primitive::get_shading_normal (primitive.cpp:86-105)
     V3 n0{a0.x, a0.y, a0.z}, n1{a0.w, a1.x, a1.y}, n2{a1.z, a1.w, a2.x};
     V3 lz = rtv::normal(rtv::add(rtv::add(rtv::mul(n0, w), rtv::mul(n1, u)), rtv::mul(n2, v)));
     V3 N = lz;
-    if (mt[1] >= 0) {
+    if (mt_n >= 0) {
         const float4 g0 = sc.tri_tan[3 * id], g1 = sc.tri_tan[3 * id + 1], g2 = sc.tri_tan[3 * id + 2];
         V3 t0{g0.x, g0.y, g0.z}, t1{g1.x, g1.y, g1.z}, tt2{g2.x, g2.y, g2.z};
         V3 lx = rtv::normal(mul_vector_d(sc.mesh_nt + 16 * mesh,
                                          rtv::normal(rtv::add(rtv::add(rtv::mul(t0, w), rtv::mul(t1, u)), rtv::mul(tt2, v)))));
         V3 ly = rtv::mul(rtv::cross(lz, lx), g0.w);
-        V3 s = rtv::reduce(tex_sample(sc, mt[1], tc, false));
+        V3 s = rtv::reduce(tex_sample_ti(sc, ti_n, tc, false));
         V3 ln = rtv::mul(rtv::addf(s, -0.5f), 2.f);
         N = rtv::normal(rtv::add(rtv::add(rtv::mul(lx, ln.x), rtv::mul(ly, ln.y)), rtv::mul(lz, ln.z)));
     }
@@ -655,8 +665,8 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     RT_PROF_SEG(1);
     // Primitive::get_metallic_roughness (primitive.cpp:131-140)
     float r2 = mf[7], metallic = mf[6];
-    if (mt[2] >= 0) {
-        V4 mr = tex_sample(sc, mt[2], tc, false);
+    if (mt_mr >= 0) {
+        V4 mr = tex_sample_ti(sc, ti_mr, tc, false);
         float rr = mr.y * mr.y;
         r2 = rr * mf[7];
         metallic = mr.z * mf[6];
@@ -707,6 +717,35 @@ __device__ __forceinline__ V3 fold_path(const Rec &P, int nv) {
         x = rtv::mul(x, P.get_cos(k));
         x = rtv::mul(x, P.get_alpha(k));
         c = rtv::add(P.get_e(k), x);
+    }
+    return c;
+}
+
+// fold_path over vertex records in memory: the same backward recurrence, with the records
+// read four vertices at a time (all loads of a batch issue before the first is used, one
+// round trip per batch instead of one per vertex).
+__device__ __forceinline__ V3 fold_path(const AosRec &P, int nv) {
+    if (nv == 0) return V3{0.f, 0.f, 0.f};
+    V3 c = P.get_e(nv - 1);
+    for (int hi = nv - 2; hi >= 0; hi -= 4) {
+        float4 A[4], B[4];
+        float C[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = hi - j >= 0 ? hi - j : 0;
+            A[j] = P.ab[2 * P.v(k)];
+            B[j] = P.ab[2 * P.v(k) + 1];
+            C[j] = P.c[P.v(k)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (hi - j < 0) break;
+            V3 x = rtv::mul(c, A[j].w);
+            x = rtv::mulv(x, V3{B[j].x, B[j].y, B[j].z});
+            x = rtv::mul(x, B[j].w);
+            x = rtv::mul(x, C[j]);
+            c = rtv::add(V3{A[j].x, A[j].y, A[j].z}, x);
+        }
     }
     return c;
 }
