@@ -57,11 +57,12 @@ struct rt_device_scene {
     int wf_node_cost = 150, wf_leaf_cost = 85;   // RT_WF_NODE_COST / RT_WF_LEAF_COST for that policy
     int wf_xcd = 0;                    // RT_WF_XCD: XCD-affine queue parts in extend (measured slower)
     int wf_ext_bpc = 0;                // RT_WF_EXTEND_BLOCKS_PER_CU: 0 = as many as fit
-    int mega_shade_min = 32;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
+    int mega_shade_min = 48;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
     int mega_wpe = 5;                  // RT_MEGA_WPE: minimum waves per SIMD the register allocation targets
     int mega_reorder = 1;              // RT_MEGA_REORDER: heaviest-first pixel order from the last counting render
     int mega_occ = 0;                  // RT_MEGA_OCC: resident blocks per CU for kernel 0 (0 = occupancy limit)
     int mega_order_min = 3;            // RT_MEGA_ORDER_MIN: reorder only with >= this many pixels per lane
+    int mega_tile = 0;                 // RT_MEGA_TILE: heaviest-first by T x T tiles (0 = by pixel)
     int mega_times = 0;                // RT_MEGA_TIMES: diagnostics, per-pixel finish-time percentiles
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
@@ -638,6 +639,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_MEGA_REORDER")) d->mega_reorder = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_OCC")) d->mega_occ = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_ORDER_MIN")) d->mega_order_min = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("RT_MEGA_TILE")) d->mega_tile = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_TIMES")) d->mega_times = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
@@ -989,7 +991,22 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipStreamSynchronize(stream));
                 std::vector<int> ord(g.n_pixels);
                 for (long long k = 0; k < g.n_pixels; ++k) ord[k] = (int)k;
-                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return c[a] > c[b]; });
+                if (d->mega_tile > 0) {
+                    // tiles of T x T shard pixels, heaviest tile first, scanline order inside
+                    // a tile (neighbouring queue entries stay neighbouring pixels)
+                    const int T = d->mega_tile, tw = (g.width + T - 1) / T;
+                    const long long rows = g.n_pixels / g.width;
+                    std::vector<unsigned long long> tc((size_t)tw * ((rows + T - 1) / T), 0);
+                    auto tile = [&](int p) { return (size_t)((p / g.width) / T) * tw + (p % g.width) / T; };
+                    for (long long k = 0; k < g.n_pixels; ++k) tc[tile((int)k)] += c[k];
+                    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                        const size_t ta = tile(a), tb = tile(b);
+                        if (ta == tb) return false;
+                        return tc[ta] != tc[tb] ? tc[ta] > tc[tb] : ta < tb;
+                    });
+                } else {
+                    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return c[a] > c[b]; });
+                }
                 HIP_TRY(hipMemcpy(d->order, ord.data(), sizeof(int) * g.n_pixels, hipMemcpyHostToDevice));
                 d->order_n = g.n_pixels;
                 d->order_key[0] = rank;
