@@ -58,6 +58,7 @@ struct rt_device_scene {
     int wf_xcd = 0;                    // RT_WF_XCD: XCD-affine queue parts in extend (measured slower)
     int wf_ext_bpc = 0;                // RT_WF_EXTEND_BLOCKS_PER_CU: 0 = as many as fit
     int mega_shade_min = 48;           // RT_MEGA_SHADE_MIN: kernel 0 shades once this many lanes are ready
+    int mega_trav_min = 0;             // RT_MEGA_TRAV_MIN: ... or once at most this many are traversing
     int mega_wpe = 5;                  // RT_MEGA_WPE: minimum waves per SIMD the register allocation targets
     int mega_reorder = 1;              // RT_MEGA_REORDER: heaviest-first pixel order from the last counting render
     int mega_occ = 0;                  // RT_MEGA_OCC: resident blocks per CU for kernel 0 (0 = occupancy limit)
@@ -272,7 +273,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         if (!__any(L.pix >= 0)) break;
         const int nr = __popcll(__ballot(L.state == rtd::M_READY));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
-        const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
+        // shade_min: low byte = ready lanes that trigger a shading pass; next byte = shade
+        // anyway once no more than this many lanes are still traversing
+        const bool shade_now = nr > 0 && (nr >= (shade_min & 255) || nt <= (shade_min >> 8));
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
@@ -634,7 +637,8 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_WF_COMPACT_BELOW")) d->wf_compact_below = std::atof(e);
     if (const char *e = std::getenv("RT_WF_PHASE_POLICY")) d->wf_policy = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_XCD")) d->wf_xcd = std::atoi(e);
-    if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("RT_MEGA_SHADE_MIN")) d->mega_shade_min = std::min(64, std::max(1, std::atoi(e)));
+    if (const char *e = std::getenv("RT_MEGA_TRAV_MIN")) d->mega_trav_min = std::min(64, std::max(0, std::atoi(e)));
     if (const char *e = std::getenv("RT_MEGA_WPE")) d->mega_wpe = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_REORDER")) d->mega_reorder = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_OCC")) d->mega_occ = std::max(0, std::atoi(e));
@@ -943,7 +947,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
-                               d->mega_shade_min, same ? (const int *)d->order : nullptr, cost,
+                               d->mega_shade_min | d->mega_trav_min << 8, same ? (const int *)d->order : nullptr, cost,
                                d->mega_times ? d->mega_tfin : nullptr);
             HIP_TRY(hipGetLastError());
 #ifdef RT_MEGA_PROF

@@ -98,8 +98,9 @@ __device__ __forceinline__ void load_pair(const float4 *nodes, uint32_t left, No
 // lane evaluates the same operations and the early returns become selects, so a wave does
 // not serialise on the inside / behind / outside cases.  Identical results; the entry
 // distance (a sqrt) only when DIST.
-template <bool DIST>
-__device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], const Ray &r, float &dist) {
+// The test itself; `coord` is the entry point (the inside case leaves it unused).
+__device__ __forceinline__ bool box_hit_pt(const float mn[3], const float mx[3], const Ray &r, float coord[3],
+                                           bool &inside_out) {
     const float o[3] = {r.o.x, r.o.y, r.o.z};
     const float d[3] = {r.d.x, r.d.y, r.d.z};
     const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
@@ -122,18 +123,27 @@ __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], co
     const float tw = w2 ? maxT[2] : t01;
     const bool on[3] = {(bool)(!w1 & !w2), (bool)(w1 & !w2), w2};
     bool out = tw < 0.f;
-    float coord[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float c = o[i] + tw * d[i];
         coord[i] = on[i] ? cand[i] : c;
         out = out | (!on[i] & ((c < mn[i]) | (c > mx[i])));
     }
-    if (DIST) {
-        const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
-        dist = inside ? 0.f : l;
-    }
+    inside_out = inside;
     return inside || !out;
+}
+// Entry distance of a box from box_hit_pt's results (0 from inside).
+__device__ __forceinline__ float box_dist(const float coord[3], bool inside, const Ray &r) {
+    const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
+    return inside ? 0.f : l;
+}
+template <bool DIST>
+__device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], const Ray &r, float &dist) {
+    float coord[3];
+    bool inside;
+    const bool hit = box_hit_pt(mn, mx, r, coord, inside);
+    if (DIST) dist = box_dist(coord, inside, r);
+    return hit;
 }
 
 // tri_hit() (rt_path.h; Primitive::intersect, primitive.cpp:17-57) as selects.
@@ -285,17 +295,18 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
         // dir[split axis] > 0: left child first (sign bits recomputed: cheaper than a register)
         const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
         const bool lf = (dpos >> b) & 1u;
-        NodeRec N, F;
+        // test both boxes as they are stored, then name them near / far
+        float cL[3], cR[3], cF[3];
+        bool inL, inR;
+        const bool hL = box_hit_pt(L.mn, L.mx, r, cL, inL);
+        const bool hR = box_hit_pt(R.mn, R.mx, r, cR, inR);
+        const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            N.mn[k] = lf ? L.mn[k] : R.mn[k]; N.mx[k] = lf ? L.mx[k] : R.mx[k];
-            F.mn[k] = lf ? R.mn[k] : L.mn[k]; F.mx[k] = lf ? R.mx[k] : L.mx[k];
-        }
+        for (int k = 0; k < 3; ++k) cF[k] = lf ? cR[k] : cL[k];
+        const float ef = box_dist(cF, lf ? inR : inL, r);   // the far child's entry distance
+        NodeRec N, F;
         N.a = lf ? L.a : R.a; N.b = lf ? L.b : R.b;
         F.a = lf ? R.a : L.a; F.b = lf ? R.b : L.b;
-        float en, ef;
-        const bool hn = box_hit<false>(N.mn, N.mx, r, en);
-        const bool hf = box_hit<true>(F.mn, F.mx, r, ef);
         if (hn && hf) {
             RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
             stk.put(T.sp++, make_uint2((F.a << 10) | F.b, __float_as_uint(ef)));
