@@ -23,6 +23,7 @@
 #include "rt_mega.h"
 #include "rt_quant_lut.h"
 #include "rt_scene.h"
+#include "rt_bvh_layout.h"
 
 using rtd::Counters;
 using rtd::DevScene;
@@ -239,9 +240,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     sc.lut = lut;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     uint2 spill[rtd::kStack - rtd::kLdsStack];
+#if RT_WIDE
+    uint32_t spill_c[rtd::kStack - rtd::kLdsStack];
+    rtd::LdsStack3 S{spill, spill_c};
+#else
     rtd::LdsStack S{spill};
+#endif
     const rtd::GlobalNodes nodes{sc.node};
-    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
+    const rtd::NodeRec root = rtd::load_node(rtd::mega_nodes(sc), 0);
     rtd::MegaLane L;
     L.pix = -1;
     L.state = rtd::M_IDLE;
@@ -520,45 +526,11 @@ size_t append(std::vector<uint8_t> &blob, const std::vector<T> &v, size_t pre = 
     return off;
 }
 
-// The device copy of the scene BVH is renumbered breadth-first: a node's children stay an
-// adjacent pair (right = left + 1) and leaves keep their triangle ranges, so traversal
-// visits, counters and results are unchanged, while the top levels become a prefix of the
-// array that the extend kernel keeps in LDS (rt_wavefront.h NodeCache).
-std::vector<float> bfs_nodes(const std::vector<float> &node) {
-    const size_t n = node.size() / 8;
-    std::vector<float> out(node.size());
-    if (n == 0) return out;
-    std::vector<uint32_t> order;   // old ids in new order
-    order.reserve(n);
-    order.push_back(0);
-    std::vector<uint32_t> new_id(n, 0);
-    for (size_t h = 0; h < order.size(); ++h) {
-        const uint32_t u = order[h];
-        uint32_t b;
-        std::memcpy(&b, &node[8 * u + 7], 4);
-        if (b < 3u) {
-            uint32_t a;
-            std::memcpy(&a, &node[8 * u + 6], 4);
-            new_id[a] = (uint32_t)order.size();
-            order.push_back(a);
-            new_id[a + 1] = (uint32_t)order.size();
-            order.push_back(a + 1);
-        }
-    }
-    for (size_t k = 0; k < order.size(); ++k) {
-        const uint32_t u = order[k];
-        std::memcpy(&out[8 * k], &node[8 * u], 8 * sizeof(float));
-        uint32_t b;
-        std::memcpy(&b, &node[8 * u + 7], 4);
-        if (b < 3u) {
-            uint32_t a;
-            std::memcpy(&a, &node[8 * u + 6], 4);
-            const uint32_t na = new_id[a];
-            std::memcpy(&out[8 * k + 6], &na, 4);
-        }
-    }
-    return out;
-}
+// The device copies of the scene BVH are renumbered breadth-first (rt_bvh_layout.h): a
+// node's children stay an adjacent pair (right = left + 1) and leaves keep their triangle
+// ranges, so traversal visits, counters and results are unchanged; the wide copy adds the
+// near-child prefetch word of rt_trav_wide.h.
+using rtd::bfs_nodes;
 
 // Device texture layout: texture t's texels in 4x4 tiles, tile (tx, ty) at tile index
 // ty * ceil(w/4) + tx, texel (x & 3, y & 3) at 4 * (y & 3) + (x & 3) inside it; tex_info keeps
@@ -601,8 +573,18 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (device < 0 || device >= ndev) return rt_fail(RT_ERR_DEVICE, "no HIP device " + std::to_string(device));
     HIP_TRY(hipSetDevice(device));
     std::vector<uint8_t> blob;
+    const std::vector<float> bfs = bfs_nodes(s->node);
+    std::vector<float> wide;
+    try {
+        wide = rtd::wide_nodes(bfs);
+    } catch (const std::exception &ex) {
+        return rt_fail(RT_ERR_LIMIT, ex.what());
+    }
+    // (every array starts 256-B aligned: a leaf lane's 4 x 16-B read of the last triangle
+    // stays inside the allocation)
     const size_t o_tri = append(blob, s->tri), o_attr = append(blob, s->tri_attr), o_tan = append(blob, s->tri_tan),
-                 o_node = append(blob, bfs_nodes(s->node), 32), o_light = append(blob, s->light),
+                 o_node = append(blob, bfs, 32), o_light = append(blob, s->light),
+                 o_node_w = append(blob, wide, 32),
                  o_lnode = append(blob, s->light_node), o_mf = append(blob, s->mesh_f),
                  o_mt = append(blob, s->mesh_tex), o_nt = append(blob, s->mesh_nt);
     // textures in 4x4-texel tiles (64 B, one cache line): a bilinear 2x2 footprint usually
@@ -655,6 +637,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.tri_attr = (const float4 *)(b + o_attr);
     ds.tri_tan = (const float4 *)(b + o_tan);
     ds.node = (const float4 *)(b + o_node);
+    ds.node_w = (const float4 *)(b + o_node_w);
     ds.light = (const float4 *)(b + o_light);
     ds.light_node = (const float4 *)(b + o_lnode);
     ds.mesh_f = (const float *)(b + o_mf);

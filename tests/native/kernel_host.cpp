@@ -5,6 +5,7 @@
 #include <cstring>
 #include <vector>
 #include "../../raytracing-hw_amd/csrc/rt_mega.h"
+#include "../../raytracing-hw_amd/csrc/rt_bvh_layout.h"
 #include "../../include/rt_hw.h"
 
 static rtd::DevScene make(const rt_scene_view *v) {
@@ -13,6 +14,14 @@ static rtd::DevScene make(const rt_scene_view *v) {
     s.tri_attr = (const float4 *)v->tri_attr;
     s.tri_tan = (const float4 *)v->tri_tan;
     s.node = (const float4 *)v->node;
+    // the device copies: wide breadth-first nodes (rt_bvh_layout.h), triangles padded by one
+    // (a leaf lane of trav_step_w reads 4 x 16 B per triangle)
+    static thread_local std::vector<float> wide, tri;
+    wide = rtd::wide_nodes(rtd::bfs_nodes(std::vector<float>(v->node, v->node + 8 * (size_t)v->n_nodes)));
+    tri.assign(v->tri, v->tri + 12 * (size_t)v->n_tris);
+    tri.resize(tri.size() + 12, 0.f);
+    s.node_w = (const float4 *)wide.data();
+    s.tri = (const float4 *)tri.data();
     s.light = (const float4 *)v->light;
     s.light_node = (const float4 *)v->light_node;
     s.mesh_f = v->mesh_f;
@@ -232,10 +241,11 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
     st.D = D;
     st.rec_ab = ab.data();
     st.rec_c = cv.data();
-    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
+    const rtd::NodeRec root = rtd::load_node(rtd::mega_nodes(sc), 0);
     const rtd::GlobalNodes nodes{sc.node};
     std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
     std::vector<std::vector<uint2>> stacks((size_t)waves * 64, std::vector<uint2>(rtd::kStack));
+    std::vector<std::vector<uint32_t>> stacks_c((size_t)waves * 64, std::vector<uint32_t>(rtd::kStack));
     for (auto &L : lanes) { L.pix = -1; L.state = rtd::M_IDLE; }
     std::vector<char> exhausted(waves, 0), done(waves, 0);
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -270,7 +280,11 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
             if (!any) { done[w] = 1; --live; continue; }
             const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
             for (int l = 0; l < 64; ++l) {
+#if RT_WIDE
+                rtd::ArrayStack3 S{stacks[(size_t)w * 64 + l].data(), stacks_c[(size_t)w * 64 + l].data()};
+#else
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
+#endif
                 rtd::mega_iterate<true>(W[l], shade_now, sc, g, st, spp, out, nullptr, root, S, nodes, cnt);
             }
         }

@@ -24,11 +24,10 @@ CASES = [("cornell", 33, 17, 3), ("cornell", 64, 64, 8), ("cornell_blob", 48, 48
 FAST = [("cornell", 33, 17, 3), ("cornell_blob", 48, 48, 4), ("sponza_mini", 64, 36, 4)]
 
 
-@pytest.fixture(scope="module")
-def kh(tmp_path_factory):
+def _build_kh(tmp_path_factory, *defines):
     out = str(tmp_path_factory.mktemp("kh") / "libkh.so")
     subprocess.run(["g++", "-O2", "-fno-tree-vectorize", "-fno-tree-slp-vectorize", "-ffp-contract=off", "-fopenmp",
-                    "-std=c++17", "-shared", "-fPIC", SRC, "-o", out], check=True)
+                    "-std=c++17", "-shared", "-fPIC", *defines, SRC, "-o", out], check=True)
     lib = ctypes.CDLL(out)
     V, I, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
     lib.kh_render.argtypes = [V, I, L, L, V, V, I]
@@ -40,6 +39,17 @@ def kh(tmp_path_factory):
     lib.kh_render_mega.argtypes = [V, I, I, I, I, I, I, V, V]
     lib.kh_render_mega.restype = I
     return lib
+
+
+@pytest.fixture(scope="module")
+def kh(tmp_path_factory):
+    return _build_kh(tmp_path_factory)
+
+
+@pytest.fixture(scope="module")
+def kh_wide(tmp_path_factory):
+    """The lane-resident kernel with the two-level traversal step (rt_trav_wide.h, RT_WIDE=1)."""
+    return _build_kh(tmp_path_factory, "-DRT_WIDE=1")
 
 
 def _golden(name, w, h, s):
@@ -150,5 +160,20 @@ def test_lane_resident_emulation(rt, kh, name, w, h, s, waves, shade_min):
     out = np.zeros((h * w, 3), np.float32)
     cnt = np.zeros(7, np.uint64)
     assert kh.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data, cnt.ctypes.data) == 0
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert list(cnt[:6]) == list(cnt_want)
+
+
+@pytest.mark.parametrize("name,w,h,s,waves,shade_min", [("cornell_blob", 48, 48, 4, 2, 32), ("sponza_mini", 64, 36, 4, 3, 1),
+                                                        ("cornell", 64, 64, 8, 2, 48)])
+def test_lane_resident_wide_traversal(rt, kh_wide, name, w, h, s, waves, shade_min):
+    """RT_WIDE=1: two node levels / two triangles per iteration from the wide breadth-first
+    node array (rt_bvh_layout.h); bit-exact sums and reference counters."""
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    out = np.zeros((h * w, 3), np.float32)
+    cnt = np.zeros(7, np.uint64)
+    assert kh_wide.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data,
+                                  cnt.ctypes.data) == 0
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert list(cnt[:6]) == list(cnt_want)
