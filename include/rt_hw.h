@@ -156,6 +156,11 @@ const char *rt_last_error(void);
 int32_t rt_abi_version(void);
 int32_t rt_device_count(void);
 int rt_device_synchronize(void);
+/* Device self-check of hardware-dependent arithmetic the kernels rely on for exactness
+ * (no reference counterpart; test entry).  which 0: the traversal's fast reciprocal
+ * (rt_wavefront.h rcp_ieee) against IEEE division over every float with a normal
+ * reciprocal; *mismatches = floats that differ (0 = exact). */
+int rt_device_selfcheck(int32_t which, uint64_t *mismatches);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,7 @@ ABI = {
     "rt_abi_version": (ctypes.c_int32, []),
     "rt_device_count": (ctypes.c_int32, []),
     "rt_device_synchronize": (ctypes.c_int, []),
+    "rt_device_selfcheck": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _lib_handle = None
@@ -295,3 +296,11 @@ def write_ppm(filename, rgb):
 
 def device_count():
     return int(lib().rt_device_count())
+
+
+def device_selfcheck(which=0):
+    """rt_device_selfcheck: mismatches of the kernels' hardware-dependent exact arithmetic
+    (0: the fast reciprocal over every float with a normal reciprocal)."""
+    n = ctypes.c_uint64(0)
+    _check(lib().rt_device_selfcheck(which, ctypes.byref(n)))
+    return int(n.value)

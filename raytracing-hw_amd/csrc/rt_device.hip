@@ -1165,6 +1165,40 @@ int rt_debug_take(unsigned long long *word) {
 }
 #endif
 
+// rt_device_selfcheck 0: rcp_ieee against the IEEE division 1.f / x over every float x
+// with a normal reciprocal path (|x| in [2^-126, 2^125)), on the device.
+__global__ void __launch_bounds__(256) rcp_check_kernel(unsigned long long *bad) {
+    unsigned long long local = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float x = __uint_as_float((uint32_t)i);
+        const float ax = fabsf(x);
+        if (!(ax >= 0x1p-126f && ax < 0x1p125f)) continue;
+        const float a = rtd::rcp_ieee(x), b = 1.f / x;
+        local += __float_as_uint(a) != __float_as_uint(b);
+    }
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
+}
+
+int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
+    if (!mismatches) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: null output");
+    if (which != 0) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
+    unsigned long long *d = nullptr;
+    HIP_TRY(hipMalloc((void **)&d, sizeof *d));
+    hipError_t e = hipMemset(d, 0, sizeof *d);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
+        e = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return rt_fail(RT_ERR_DEVICE, std::string("rt_device_selfcheck: ") + hipGetErrorString(e));
+    *mismatches = h;
+    return RT_OK;
+}
+
 int32_t rt_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

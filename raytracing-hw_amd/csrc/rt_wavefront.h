@@ -146,12 +146,80 @@ __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], co
     return hit;
 }
 
+// Both boxes of a child pair at once: the same operations as box_hit_pt on each, arranged
+// for fewer instructions:
+//   * the candidate plane is `lo ? min : max`: box_hit_pt's 0 for a Mid axis is never
+//     used (a Mid axis has maxT = -1 and only wins when the box is missed);
+//   * dir != 0 is tested once for both boxes;
+//   * the entry point is selected only for the far box (`lf`: the left box is the near one),
+//     the only one whose distance traversal needs.
+__device__ __forceinline__ void box_pair_hit(const NodeRec &L, const NodeRec &R, const Ray &r, bool lf, bool &hL, bool &hR,
+                                             float coordF[3], bool &insideF) {
+    const float o[3] = {r.o.x, r.o.y, r.o.z};
+    const float d[3] = {r.d.x, r.d.y, r.d.z};
+    const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+    bool inL = true, inR = true;
+    float candL[3], candR[3], mtL[3], mtR[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const bool loL = o[i] < L.mn[i], loR = o[i] < R.mn[i];
+        const bool midL = !loL & !(o[i] > L.mx[i]), midR = !loR & !(o[i] > R.mx[i]);
+        inL = inL & midL;
+        inR = inR & midR;
+        candL[i] = loL ? L.mn[i] : L.mx[i];
+        candR[i] = loR ? R.mn[i] : R.mx[i];
+        const bool dnz = d[i] != 0.f;
+        const float tL = (candL[i] - o[i]) * inv[i], tR = (candR[i] - o[i]) * inv[i];
+        mtL[i] = (!midL & dnz) ? tL : -1.f;
+        mtR[i] = (!midR & dnz) ? tR : -1.f;
+    }
+    const bool w1L = mtL[0] < mtL[1], w1R = mtR[0] < mtR[1];
+    const float t01L = w1L ? mtL[1] : mtL[0], t01R = w1R ? mtR[1] : mtR[0];
+    const bool w2L = t01L < mtL[2], w2R = t01R < mtR[2];
+    const float twL = w2L ? mtL[2] : t01L, twR = w2R ? mtR[2] : t01R;
+    const bool onL[3] = {(bool)(!w1L & !w2L), (bool)(w1L & !w2L), w2L};
+    const bool onR[3] = {(bool)(!w1R & !w2R), (bool)(w1R & !w2R), w2R};
+    bool outL = twL < 0.f, outR = twR < 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float cL = o[i] + twL * d[i], cR = o[i] + twR * d[i];
+        outL = outL | (!onL[i] & ((cL < L.mn[i]) | (cL > L.mx[i])));
+        outR = outR | (!onR[i] & ((cR < R.mn[i]) | (cR > R.mx[i])));
+        coordF[i] = lf ? (onR[i] ? candR[i] : cR) : (onL[i] ? candL[i] : cL);
+    }
+    hL = inL || !outL;
+    hR = inR || !outR;
+    insideF = lf ? inR : inL;
+}
+
+// 1.f / x, correctly rounded, in three instructions where that is exact: the hardware
+// reciprocal (about 1 ulp) and one fma Newton correction, which rounds correctly for every
+// normal x with a normal reciprocal — checked on the device over every such float
+// (rt_device_selfcheck 0, tests/test_gpu_parity.py).  Other x (denormal or huge, inf, NaN)
+// take the IEEE division in a branch no real triangle reaches.  The host build divides.
+__device__ __forceinline__ float rcp_ieee(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float ax = __builtin_fabsf(x);
+    const float y0 = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y0, 1.f);
+    float y = __builtin_fmaf(e, y0, y0);
+    if (__builtin_expect(!((ax >= 0x1p-126f) & (ax < 0x1p125f)), 0)) y = 1.f / x;
+    return y;
+#else
+    return 1.f / x;
+#endif
+}
+
 // tri_hit() (rt_path.h; Primitive::intersect, primitive.cpp:17-57) as selects.
 __device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriHit &h) {
     const V3 p = rtv::cross(r.d, V);
     const float det = rtv::dot(U, p);
     const bool ok_det = !((-1e-6 < (double)det) & ((double)det < 1e-6));
+#if RT_FAST_RCP
+    const float inv_det = rcp_ieee(det);
+#else
     const float inv_det = 1.f / det;
+#endif
     const V3 s = rtv::sub(r.o, v0);
     const float u = inv_det * rtv::dot(s, p);
     const V3 q = rtv::cross(s, U);
@@ -207,6 +275,14 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
     q[kQRec * (size_t)p] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
 }
 
+// tri_hit_bl's 1 / det by rcp_ieee (compile-time A/B knob; 0 = the compiler's IEEE division).
+#ifndef RT_FAST_RCP
+#define RT_FAST_RCP 1
+#endif
+// trav_step tests a child pair with box_pair_hit (compile-time A/B knob; 0 = box_hit_pt twice).
+#ifndef RT_BOX_PAIR
+#define RT_BOX_PAIR 1
+#endif
 // trav_step issues the node-pair and triangle reads together (compile-time A/B knob).
 #ifndef RT_HOIST_LOADS
 #define RT_HOIST_LOADS 1
@@ -296,14 +372,21 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
         const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
         const bool lf = (dpos >> b) & 1u;
         // test both boxes as they are stored, then name them near / far
-        float cL[3], cR[3], cF[3];
+        float cF[3];
+#if RT_BOX_PAIR
+        bool hL, hR, inF;
+        box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
+        const float ef = box_dist(cF, inF, r);   // the far child's entry distance
+#else
+        float cL[3], cR[3];
         bool inL, inR;
         const bool hL = box_hit_pt(L.mn, L.mx, r, cL, inL);
         const bool hR = box_hit_pt(R.mn, R.mx, r, cR, inR);
-        const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
 #pragma unroll
         for (int k = 0; k < 3; ++k) cF[k] = lf ? cR[k] : cL[k];
         const float ef = box_dist(cF, lf ? inR : inL, r);   // the far child's entry distance
+#endif
+        const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
         NodeRec N, F;
         N.a = lf ? L.a : R.a; N.b = lf ? L.b : R.b;
         F.a = lf ? R.a : L.a; F.b = lf ? R.b : L.b;

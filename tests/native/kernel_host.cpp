@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 #include "../../raytracing-hw_amd/csrc/rt_mega.h"
 #include "../../raytracing-hw_amd/csrc/rt_bvh_layout.h"
 #include "../../include/rt_hw.h"
@@ -292,4 +293,56 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
     uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
     std::memcpy(cnt_out, c, sizeof c);
     return 0;
+}
+
+// box_pair_hit (rt_wavefront.h) against box_hit_pt on each box of the pair, over `n`
+// random cases drawn from a small set of special values (planes through the origin,
+// signed zeros, infinities, NaN, inverted boxes) mixed with ordinary floats.  Returns the
+// number of mismatching cases (hit flags, far-box inside flag, far-box entry distance bits;
+// any NaN distance equals any other: traversal only compares it).
+extern "C" long long kh_box_pair_check(long long n, uint32_t seed) {
+    uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto next = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    const float specials[] = {0.f, -0.f, 1.f, -1.f, 0.5f, -2.f, 1e-30f, -1e-30f, 1e30f, -1e30f, 1e-45f,
+                              __builtin_inff(), -__builtin_inff(), __builtin_nanf("")};
+    auto val = [&]() -> float {
+        const uint64_t r = next();
+        if ((r & 3) == 0) return specials[(r >> 8) % (sizeof specials / sizeof specials[0])];
+        return ((float)((r >> 16) & 0xffff) / 32768.f - 1.f) * 4.f;
+    };
+    long long bad = 0;
+    for (long long k = 0; k < n; ++k) {
+        rtd::Ray r;
+        r.o = rtv::V3{val(), val(), val()};
+        r.d = rtv::V3{val(), val(), val()};
+        r.inv = rtv::V3{1.f / r.d.x, 1.f / r.d.y, 1.f / r.d.z};
+        rtd::NodeRec L{}, R{};
+        for (int i = 0; i < 3; ++i) {
+            const float a = val(), b = val(), c = val(), e = val();
+            const bool inv_box = (next() & 15) == 0;   // occasionally inverted
+            L.mn[i] = inv_box ? std::max(a, b) : std::min(a, b);
+            L.mx[i] = inv_box ? std::min(a, b) : std::max(a, b);
+            R.mn[i] = std::min(c, e);
+            R.mx[i] = (next() & 7) == 0 ? R.mn[i] : std::max(c, e);   // flat boxes too
+            const float oi = i == 0 ? r.o.x : (i == 1 ? r.o.y : r.o.z);
+            if ((next() & 7) == 0 && oi <= R.mx[i]) R.mn[i] = oi;   // plane through the origin
+        }
+        const bool lf = next() & 1;
+        float cL[3], cR[3], cF[3];
+        bool inL, inR, hL, hR, inF;
+        const bool wL = rtd::box_hit_pt(L.mn, L.mx, r, cL, inL);
+        const bool wR = rtd::box_hit_pt(R.mn, R.mx, r, cR, inR);
+        rtd::box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
+        bool ok = wL == hL && wR == hR && inF == (lf ? inR : inL);
+        const bool far_hit = lf ? wR : wL;
+        if (ok && far_hit) {   // the entry distance is only used for a hit far box
+            const float want = rtd::box_dist(lf ? cR : cL, lf ? inR : inL, r), got = rtd::box_dist(cF, inF, r);
+            uint32_t a, b;
+            std::memcpy(&a, &want, 4);
+            std::memcpy(&b, &got, 4);
+            ok = ok && (a == b || (want != want && got != got));   // (traversal only compares it)
+        }
+        bad += !ok;
+    }
+    return bad;
 }

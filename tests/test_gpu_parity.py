@@ -166,3 +166,9 @@ def test_device_finish_matches_reference(gpu):
     gpu.tonemap_device(d_sum.data_ptr(), 200, 300, 16, d_rgb.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(d_rgb.cpu().numpy().reshape(300, 200, 3), host)
+
+
+def test_fast_reciprocal_is_exact(gpu):
+    """The traversal's 1/det (rt_wavefront.h rcp_ieee: v_rcp_f32 + one fma correction) equals
+    the IEEE division for every float with a normal reciprocal (2^32 values on the device)."""
+    assert gpu.device_selfcheck(0) == 0

@@ -38,6 +38,8 @@ def _build_kh(tmp_path_factory, *defines):
     lib.kh_render_wf.restype = I
     lib.kh_render_mega.argtypes = [V, I, I, I, I, I, I, V, V]
     lib.kh_render_mega.restype = I
+    lib.kh_box_pair_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
+    lib.kh_box_pair_check.restype = ctypes.c_int64
     return lib
 
 
@@ -177,3 +179,10 @@ def test_lane_resident_wide_traversal(rt, kh_wide, name, w, h, s, waves, shade_m
                                   cnt.ctypes.data) == 0
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert list(cnt[:6]) == list(cnt_want)
+
+
+def test_box_pair_matches_single_box_test(kh):
+    """box_pair_hit (the traversal's pair test) agrees with box_hit_pt (AABB::intersect,
+    primitive.cpp:146-208, restated op for op) on 4 M random cases rich in special values:
+    signed zeros, infinities, NaN, flat and inverted boxes, planes through the origin."""
+    assert kh.kh_box_pair_check(4_000_000, 7) == 0
