@@ -890,6 +890,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const long long need = (g.n_pixels + 255) / 256;
             unsigned blocks = (unsigned)std::min<long long>(need, (long long)d->cu_count * per_cu);
             if (blocks == 0) blocks = 1;
+            w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity: blocks <= need)
             // pixel order: heaviest first, from the per-pixel costs of the last counting render of
             // this shard (the frame's tail is then made of cheap pixels); natural order otherwise
             // (only with >= 3 pixels per lane: with fewer, every lane starts at once and sorting

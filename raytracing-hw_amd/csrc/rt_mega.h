@@ -14,7 +14,7 @@
 //     shading code serves many lanes);
 //   * a lane whose pixel has all its samples takes the next pixel from a per-launch queue.
 // RNG, pixel sum, sample counter and depth budget live in registers; the vertex records go
-// to HBM (AosRec, indexed by pixel).  Same per-pixel arithmetic, so bit-identical output.
+// to memory (LaneRec, indexed by lane slot).  Same per-pixel arithmetic, so bit-identical output.
 #pragma once
 #include "rt_wavefront.h"
 #include "rt_trav_wide.h"
@@ -28,7 +28,20 @@
 #define RT_WIDE 0
 #endif
 
+// RT_LANE_RECORDS: vertex records by lane slot (LaneRec) instead of by pixel (AosRec).
+#ifndef RT_LANE_RECORDS
+#define RT_LANE_RECORDS 1
+#endif
+
 namespace rtd {
+
+// The lane's slot: its global thread index (the host emulation sets it per lane).
+#if defined(__HIPCC__)
+__device__ __forceinline__ long long mega_slot() { return (long long)blockIdx.x * blockDim.x + threadIdx.x; }
+#else
+inline thread_local long long g_mega_slot = 0;
+inline long long mega_slot() { return g_mega_slot; }
+#endif
 
 #if RT_WIDE
 using MegaTrav = TravW;
@@ -92,7 +105,11 @@ __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, con
 template <bool COUNT>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Counters &cnt) {
+#if RT_LANE_RECORDS
+    LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
+#else
     AosRec P{st.rec_ab, st.rec_c, L.pix, st.D, V3{0.f, 0.f, 0.f}, 0, false};
+#endif
     const Hit h = L.T.best;
     bool next = false;
     if (h.prim >= 0 && h.t < sc.max_distance && shade_hit<COUNT>(sc, L.r, h, L.rng, cnt, P, L.nv) && L.power > 0) {

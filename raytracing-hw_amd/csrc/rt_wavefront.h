@@ -24,6 +24,7 @@ struct WfState {
     float4 *st;       // 2 per slot: (rng state bits, normal cache, meta bits, 0), (pixel sum, 0)
     float4 *rec_ab;   // AosRec: 2 per slot and vertex
     float *rec_c;     //         1 per slot and vertex
+    long long lanes;  // lane-resident kernel: lane slots (LaneRec stride; rt_path.h)
 };
 // meta: samples done (bits 0-19), depth budget left (20-23), vertices recorded (24-27),
 // normal cache valid (28)

@@ -235,13 +235,15 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
     const long long n = (long long)rows * v->width;
     rtd::ShardGeom g{v->width, rank, world, row_block, n};
     const int D = v->ray_depth;
-    std::vector<float4> ab((size_t)2 * n * D);
-    std::vector<float> cv((size_t)n * D);
+    const long long slots = std::max<long long>(n, (long long)waves * 64);
+    std::vector<float4> ab((size_t)2 * slots * D);
+    std::vector<float> cv((size_t)slots * D);
     rtd::WfState st{};
     st.n = n;
     st.D = D;
     st.rec_ab = ab.data();
     st.rec_c = cv.data();
+    st.lanes = (long long)waves * 64;
     const rtd::NodeRec root = rtd::load_node(rtd::mega_nodes(sc), 0);
     const rtd::GlobalNodes nodes{sc.node};
     std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
@@ -286,6 +288,7 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
 #else
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
 #endif
+                rtd::g_mega_slot = (long long)w * 64 + l;
                 rtd::mega_iterate<true>(W[l], shade_now, sc, g, st, spp, out, nullptr, root, S, nodes, cnt);
             }
         }
