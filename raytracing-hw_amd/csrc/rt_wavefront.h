@@ -193,6 +193,11 @@ __device__ __forceinline__ void box_pair_hit(const NodeRec &L, const NodeRec &R,
     insideF = lf ? inR : inL;
 }
 
+// tri_hit_bl's 1 / det by rcp_ieee (compile-time A/B knob; 0 = the compiler's IEEE division).
+#ifndef RT_FAST_RCP
+#define RT_FAST_RCP 1
+#endif
+
 // 1.f / x, correctly rounded, in three instructions where that is exact: the hardware
 // reciprocal (about 1 ulp) and one fma Newton correction, which rounds correctly for every
 // normal x with a normal reciprocal — checked on the device over every such float
@@ -215,7 +220,9 @@ __device__ __forceinline__ float rcp_ieee(float x) {
 __device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriHit &h) {
     const V3 p = rtv::cross(r.d, V);
     const float det = rtv::dot(U, p);
-    const bool ok_det = !((-1e-6 < (double)det) & ((double)det < 1e-6));
+    // -1e-6 < (double)det < 1e-6 in float: 0x1.0c6f7cp-20f is the least float above the double
+    // 1e-6, so the double compares and |det| < it agree on every float (NaN included)
+    const bool ok_det = !(__builtin_fabsf(det) < 0x1.0c6f7cp-20f);
 #if RT_FAST_RCP
     const float inv_det = rcp_ieee(det);
 #else
@@ -276,10 +283,6 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
     q[kQRec * (size_t)p] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
 }
 
-// tri_hit_bl's 1 / det by rcp_ieee (compile-time A/B knob; 0 = the compiler's IEEE division).
-#ifndef RT_FAST_RCP
-#define RT_FAST_RCP 1
-#endif
 // trav_step tests a child pair with box_pair_hit (compile-time A/B knob; 0 = box_hit_pt twice).
 #ifndef RT_BOX_PAIR
 #define RT_BOX_PAIR 1

@@ -1,0 +1,24 @@
+#!/bin/bash
+# SQ counter passes over one rank's shard (tools/shard_time.py) per world size, to compare
+# where wave time goes at full and at low occupancy.  One rocprofv3 --pmc pass per run.
+#   bash tools/pmc_shard.sh TAG "8 128" [pass ...]        (passes: sq1 sq2; default both)
+set -o pipefail
+cd "$(dirname "$0")/.."
+TAG=$1; WORLDS=$2; shift 2
+PASSES=${*:-sq1 sq2}
+OUT=gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for w in $WORLDS; do
+  for p in $PASSES; do
+    case $p in
+      sq1) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CYCLES" ;;
+      sq2) C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INST_LEVEL_VMEM SQ_INSTS_LDS" ;;
+      sq3) C="SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_EXP SQ_LDS_BANK_CONFLICT" ;;
+    esac
+    timeout -s KILL 150 rocprofv3 --pmc $C -d "$OUT/${p}_w$w" -o run -- python3 tools/shard_time.py --worlds $w --steps 1 \
+        > "$OUT/${p}_w$w.log" 2>&1 || { echo "pass $p w$w failed"; exit 1; }
+    python3 tools/rocpd_summary.py pmc "$OUT/${p}_w$w/run_results.db" "$OUT/${p}_w$w.csv" || exit 1
+    echo "[pmc] $p w$w done"
+  done
+done
