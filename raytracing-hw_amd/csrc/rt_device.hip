@@ -66,6 +66,8 @@ struct rt_device_scene {
     int mega_order_min = 3;            // RT_MEGA_ORDER_MIN: reorder only with >= this many pixels per lane
     int mega_tile = 0;                 // RT_MEGA_TILE: heaviest-first by T x T tiles (0 = by pixel)
     int mega_times = 0;                // RT_MEGA_TIMES: diagnostics, per-pixel finish-time percentiles
+    int mega_spread = 1;               // RT_MEGA_SPREAD: first pixels of a wave's lanes from different cost strata
+    int mega_fill = 0;                 // RT_MEGA_FILL: fewer pixels than lanes -> every resident wave, fewer lanes each
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
     // that order (per shard geometry): pixel indices by descending traversal work
@@ -252,6 +254,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     L.pix = -1;
     L.state = rtd::M_IDLE;
     bool exhausted = false;
+    // lanes of the wave that take pixels (bits 16-22 of shade_min; 0 = all 64)
+    const int lane_cap = (shade_min >> 16) & 127 ? (shade_min >> 16) & 127 : 64;
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -260,7 +264,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 #endif
     for (;;) {
         if (!exhausted) {   // lanes without a pixel take the next ones (one atomic per wave)
-            const bool need = L.pix < 0;
+            const bool need = L.pix < 0 && lane < lane_cap;
             const unsigned long long m = __ballot(need);
             if (m) {
                 const int leader = __ffsll((unsigned long long)m) - 1;
@@ -281,7 +285,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
         // shade_min: low byte = ready lanes that trigger a shading pass; next byte = shade
         // anyway once no more than this many lanes are still traversing
-        const bool shade_now = nr > 0 && (nr >= (shade_min & 255) || nt <= (shade_min >> 8));
+        const bool shade_now = nr > 0 && (nr >= (shade_min & 255) || nt <= ((shade_min >> 8) & 255));
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
@@ -627,6 +631,8 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_MEGA_ORDER_MIN")) d->mega_order_min = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_TILE")) d->mega_tile = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_MEGA_TIMES")) d->mega_times = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_SPREAD")) d->mega_spread = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_FILL")) d->mega_fill = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -870,10 +876,6 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (rc) return rc;
         } else if (p->kernel == 0) {   // lane-resident (rt_mega.h), the default
             if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "ray_depth must be in [1, 15]");
-            int rc = ensure_wf(d, g.n_pixels, s->ray_depth);   // vertex records
-            if (rc) return rc;
-            rtd::WfState w = d->wf;
-            w.n = g.n_pixels;
             auto pick = [&](int wpe) {
                 switch (wpe) {
                     case 5: return count ? rt_mega_kernel<true, 5> : rt_mega_kernel<false, 5>;
@@ -887,15 +889,33 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk, 256, 0));
             if (per_cu < 1) per_cu = 1;
             if (d->mega_occ > 0) per_cu = std::min(per_cu, d->mega_occ);
-            const long long need = (g.n_pixels + 255) / 256;
-            unsigned blocks = (unsigned)std::min<long long>(need, (long long)d->cu_count * per_cu);
+            const long long need = (g.n_pixels + 255) / 256, resident = (long long)d->cu_count * per_cu;
+            unsigned blocks = (unsigned)std::min<long long>(need, resident);
             if (blocks == 0) blocks = 1;
-            w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity: blocks <= need)
-            // pixel order: heaviest first, from the per-pixel costs of the last counting render of
-            // this shard (the frame's tail is then made of cheap pixels); natural order otherwise
-            // (only with >= 3 pixels per lane: with fewer, every lane starts at once and sorting
-            // only clusters the heavy pixels on the same SIMDs — measured slower at 4 and 8 GPUs)
-            const bool many = g.n_pixels >= (long long)d->mega_order_min * blocks * 256;
+            // RT_MEGA_FILL: with fewer pixels than resident lanes, launch every resident wave and
+            // give each ceil(pixels / waves) lanes: more, narrower waves per SIMD
+            int lane_cap = 64;
+            if (d->mega_fill && need < resident) {
+                blocks = (unsigned)resident;
+                lane_cap = (int)std::min<long long>(64, (g.n_pixels + 4LL * blocks - 1) / (4LL * blocks));
+            }
+            int rc = ensure_wf(d, std::max<long long>(g.n_pixels, (long long)blocks * 256), s->ray_depth);   // vertex records
+            if (rc) return rc;
+            rtd::WfState w = d->wf;
+            w.n = g.n_pixels;
+            w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity)
+            // pixel order, from the per-pixel costs of the last counting render of this shard
+            // (results never depend on it):
+            //   * heaviest first, so the frame's tail is made of cheap pixels;
+            //   * spread (RT_MEGA_SPREAD, default): the first claims, one pixel per lane, give
+            //     every wave one pixel of each cost stratum.  A pixel's 256 samples are one
+            //     sequential chain, and with ~1 pixel per lane (8 GPUs) the frame is the
+            //     heaviest pixel's chain; with light wave-mates that finish early, it runs in a
+            //     sparse wave (fewer divergent paths per iteration, shading batches not held
+            //     back).  Rank-0 shard of an 8-way split: 490 -> 353 ms; 1 GPU: +1-2%.
+            //     Plain heaviest-first (RT_MEGA_SPREAD=0) only with >= RT_MEGA_ORDER_MIN pixels
+            //     per lane: with fewer it clusters the heavy pixels in the same waves.
+            const bool many = g.n_pixels >= (long long)d->mega_order_min * blocks * 256 || d->mega_spread;
             const bool same = many && d->order && d->order_n == g.n_pixels && d->order_key[0] == rank &&
                               d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && d->mega_reorder;
             unsigned *cost = nullptr;
@@ -931,7 +951,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
-                               d->mega_shade_min | d->mega_trav_min << 8, same ? (const int *)d->order : nullptr, cost,
+                               d->mega_shade_min | d->mega_trav_min << 8 | (lane_cap & 127) << 16,
+                               same ? (const int *)d->order : nullptr, cost,
                                d->mega_times ? d->mega_tfin : nullptr);
             HIP_TRY(hipGetLastError());
 #ifdef RT_MEGA_PROF
@@ -994,6 +1015,21 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                     });
                 } else {
                     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return c[a] > c[b]; });
+                }
+                if (d->mega_spread) {
+                    // the first claims (one per lane: every wave takes lane_cap consecutive queue
+                    // entries at its start) get the heaviest pixels, but each wave one pixel of
+                    // every cost stratum, so a heavy pixel's wave-mates are light and finish early;
+                    // later claims stay heaviest-first
+                    const long long groups = 4LL * blocks, first = std::min<long long>(g.n_pixels, groups * lane_cap);
+                    std::vector<int> sp(ord);
+                    long long r = 0;
+                    for (long long j = 0; j < lane_cap; ++j)
+                        for (long long gi = 0; gi < groups; ++gi) {
+                            const long long q = gi * lane_cap + j;
+                            if (q < first) sp[q] = ord[r++];
+                        }
+                    ord.swap(sp);
                 }
                 HIP_TRY(hipMemcpy(d->order, ord.data(), sizeof(int) * g.n_pixels, hipMemcpyHostToDevice));
                 d->order_n = g.n_pixels;

@@ -291,6 +291,15 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
 #ifndef RT_HOIST_LOADS
 #define RT_HOIST_LOADS 1
 #endif
+// Leaf triangles tested per trav_step (1-4; node arrays in plain memory only).  A node lane
+// and a leaf lane read through the same registers: 4 x 16 B of the child pair, or of
+// triangle k (its 3 x 16 B and the next record's first), then 3 x 16 B per further triangle.
+// Sponza 1080p x256spp, lane-resident kernel: 2 is +3.6% at 1 GPU and -7% on the rank-0
+// shard of an 8-way split (fewer iterations on the heaviest pixel's chain); 3 and 4 lose
+// at 1 GPU (more registers live across the step).
+#ifndef RT_LEAF_N
+#define RT_LEAF_N 2
+#endif
 
 // Resumable traversal state of one ray.
 enum TravPhase : int { TP_NODE = 0, TP_LEAF = 1, TP_POP = 2 };
@@ -305,7 +314,9 @@ struct TravState {
 
 // Where trav_step reads child pairs from: the node array in HBM ...
 struct GlobalNodes {
+    static constexpr bool kPtr = true;   // pairs are plain memory (trav_step's shared load registers)
     const float4 *node;
+    __device__ __forceinline__ const float4 *pair(uint32_t left) const { return node + 2 * (size_t)left; }
     __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
         rtd::load_pair(node, left, L, R);
     }
@@ -344,6 +355,109 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
     return (bits & 8u) == 0;
 }
 
+// The return of trav_step: merge subtree bests upwards until a far child is to be visited
+// (enter it: false) or the stack is empty (T.best is final: true).
+template <class Stack>
+__device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
+    float acc = T.acc;
+    int sp = T.sp;
+    for (;;) {
+        if (sp == 0) {
+            T.sp = 0;
+            T.acc = acc;
+            return true;
+        }
+        const uint2 f = stk.get(--sp);
+        if (f.x == kFrameAcc) {
+            const float p = __uint_as_float(f.y);
+            acc = acc < p ? acc : p;
+            continue;
+        }
+        if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
+            stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
+#ifdef RT_STACK_PROBE
+            RT_STACK_PROBE(sp);
+#endif
+            T.sp = sp;
+            T.acc = 1e9f;
+            trav_enter(T, f.x >> 10, f.x & 1023u);
+            return false;
+        }
+    }
+}
+
+// trav_step with RT_LEAF_N triangles per leaf step (see RT_LEAF_N).  Same node step, same
+// frames; a leaf lane tests triangles k .. k + N - 1 of its leaf in the reference's order
+// (strict <, so the first of equal t wins), which is the sequence of N single steps.
+template <bool COUNT, class Stack, class Nodes>
+__device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
+                                            const Nodes &nodes, Counters &cnt, bool at_node, bool at_leaf) {
+    constexpr int N = RT_LEAF_N;
+    const uint32_t k = T.k, klast = T.kend - 1u;
+    RT_CHECK(!at_node || T.a + 1 < (uint32_t)sc.n_nodes, 10, T.a, T.a = 0);
+    RT_CHECK(!at_leaf || T.kend <= (uint32_t)sc.n_tris, 12, T.kend, T.k = T.kend = 1);
+    float4 q[4 + 3 * (N - 1)];
+    {
+        const float4 *p0 = at_node ? nodes.pair(T.a) : sc.tri + 3 * (size_t)(at_leaf ? k : 0u);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = p0[i];
+#pragma unroll
+        for (int j = 1; j < N; ++j) {
+            const uint32_t kj = at_leaf ? (k + j < klast ? k + j : klast) : 0u;
+            const float4 *pj = sc.tri + 3 * (size_t)kj;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) q[4 + 3 * (j - 1) + i] = pj[i];
+        }
+#ifdef __HIPCC__
+        asm volatile("" ::"v"(q[0].x), "v"(q[1].y), "v"(q[2].z), "v"(q[3].w));
+#endif
+    }
+    if (at_node) {
+        NodeRec L, R;
+        L.mn[0] = q[0].x; L.mn[1] = q[0].y; L.mn[2] = q[0].z; L.mx[0] = q[0].w; L.mx[1] = q[1].x; L.mx[2] = q[1].y;
+        L.a = __float_as_uint(q[1].z); L.b = __float_as_uint(q[1].w);
+        R.mn[0] = q[2].x; R.mn[1] = q[2].y; R.mn[2] = q[2].z; R.mx[0] = q[2].w; R.mx[1] = q[3].x; R.mx[2] = q[3].y;
+        R.a = __float_as_uint(q[3].z); R.b = __float_as_uint(q[3].w);
+        if (COUNT) cnt.aabb += 2;
+        const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
+        const bool lf = (dpos >> T.b) & 1u;
+        float cF[3];
+        bool hL, hR, inF;
+        box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
+        const float ef = box_dist(cF, inF, r);
+        const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
+        const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
+        if (hn && hf) {
+            RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
+            stk.put(T.sp++, make_uint2((fa << 10) | fb, __float_as_uint(ef)));
+#ifdef RT_STACK_PROBE
+            RT_STACK_PROBE(T.sp);
+#endif
+        }
+        const bool far_only = !hn && hf && !(ef > 1e9f);
+        if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
+        else T.phase = TP_POP;
+    } else if (at_leaf) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int o = j == 0 ? 0 : 4 + 3 * (j - 1);
+            const V3 v0{q[o].x, q[o].y, q[o].z}, U{q[o].w, q[o + 1].x, q[o + 1].y}, V{q[o + 1].z, q[o + 1].w, q[o + 2].x};
+            const bool valid = j == 0 || k + j <= klast;
+            TriHit h;
+            const bool hit = tri_hit_bl(v0, U, V, r, h) & valid;
+            if (COUNT && valid) cnt.tri++;
+            if (hit) {
+                T.acc = h.t < T.acc ? h.t : T.acc;
+                if (h.t < T.best.t) { T.best.t = h.t; T.best.u = h.u; T.best.v = h.v; T.best.prim = (int)(k + j); }
+            }
+        }
+        T.k = k + N;
+        if (T.k >= T.kend) T.phase = TP_POP;
+    }
+    if (T.phase == TP_POP) return trav_pop(T, stk);
+    return false;
+}
+
 // One unit of traversal work: the child pair of one internal node, or one leaf triangle,
 // followed (when the subtree is finished) by the return up the frames until a far child
 // is to be visited.  Returns true once the stack is empty (T.best is final).  A wave's
@@ -352,6 +466,7 @@ template <bool COUNT, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, const Nodes &nodes,
                                           Counters &cnt) {
     const bool at_node = T.phase == TP_NODE, at_leaf = T.phase == TP_LEAF;
+    if constexpr (RT_LEAF_N > 1 && Nodes::kPtr) return trav_step_n<COUNT>(sc, r, T, stk, nodes, cnt, at_node, at_leaf);
     NodeRec L, R;
     V3 v0, U, V;
 #if RT_HOIST_LOADS
@@ -484,6 +599,7 @@ struct LdsStack {
 constexpr int kLdsNodes = 128;   // 4 KB: the top 7 levels of a full tree
 __shared__ float4 wf_lds_nodes[2 * kLdsNodes];
 struct LdsNodes {
+    static constexpr bool kPtr = false;
     const float4 *node;
     __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
         if (left + 1 < (uint32_t)kLdsNodes) {

@@ -181,6 +181,22 @@ def test_lane_resident_wide_traversal(rt, kh_wide, name, w, h, s, waves, shade_m
     assert list(cnt[:6]) == list(cnt_want)
 
 
+@pytest.mark.parametrize("leaf_n", [1, 3, 4])
+def test_lane_resident_leaf_triangles(rt, tmp_path_factory, leaf_n):
+    """RT_LEAF_N (default 2, covered by the tests above): 1, 3 or 4 triangles of a leaf per
+    traversal step through the shared load registers; bit-exact sums and reference counters."""
+    kh_n = _build_kh(tmp_path_factory, f"-DRT_LEAF_N={leaf_n}")
+    for name, w, h, s, waves, shade_min in [("cornell_blob", 48, 48, 4, 2, 32), ("sponza_mini", 64, 36, 4, 3, 1)]:
+        want, cnt_want = _golden(name, w, h, s)
+        v, keep = _view(rt, name, w, h, s)
+        out = np.zeros((h * w, 3), np.float32)
+        cnt = np.zeros(7, np.uint64)
+        assert kh_n.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data,
+                                   cnt.ctypes.data) == 0
+        assert np.array_equal(rtref.bits(out), rtref.bits(want))
+        assert list(cnt[:6]) == list(cnt_want)
+
+
 def test_box_pair_matches_single_box_test(kh):
     """box_pair_hit (the traversal's pair test) agrees with box_hit_pt (AABB::intersect,
     primitive.cpp:146-208, restated op for op) on 4 M random cases rich in special values:
