@@ -67,6 +67,7 @@ struct rt_device_scene {
     int mega_tile = 0;                 // RT_MEGA_TILE: heaviest-first by T x T tiles (0 = by pixel)
     int mega_times = 0;                // RT_MEGA_TIMES: diagnostics, per-pixel finish-time percentiles
     int mega_spread = 1;               // RT_MEGA_SPREAD: first pixels of a wave's lanes from different cost strata
+    int mega_team = 1;                 // RT_MEGA_TEAM (builds with RT_TEAM=1): a wave's last traversing pixel walked by all its lanes
     int mega_fill = 0;                 // RT_MEGA_FILL: fewer pixels than lanes -> every resident wave, fewer lanes each
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
@@ -256,6 +257,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     bool exhausted = false;
     // lanes of the wave that take pixels (bits 16-22 of shade_min; 0 = all 64)
     const int lane_cap = (shade_min >> 16) & 127 ? (shade_min >> 16) & 127 : 64;
+    const bool team = (shade_min >> 23) & 1;   // RT_MEGA_TEAM
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -286,6 +288,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         // shade_min: low byte = ready lanes that trigger a shading pass; next byte = shade
         // anyway once no more than this many lanes are still traversing
         const bool shade_now = nr > 0 && (nr >= (shade_min & 255) || nt <= ((shade_min >> 8) & 255));
+#if RT_TEAM && !RT_WIDE
+        // the wave's last pixel is traversing: the whole wave walks its ray (rt_team.h)
+        if (!COUNT && team && nt == 1 && nr == 0) {
+            const unsigned long long act = __ballot(L.pix >= 0);
+#ifdef RT_MEGA_PROF
+            const long long t0 = clock64();
+#endif
+            if (__popcll(act) == 1 && rtd::mega_team(L, __ffsll((unsigned long long)act) - 1, sc)) {
+#ifdef RT_MEGA_PROF
+                tp = clock64();
+                if (lane == 0) {
+                    atomicAdd(&rt_prof_lds[6], (unsigned long long)(tp - t0));
+                    atomicAdd(&rt_prof_lds[7], 1ull);
+                }
+#endif
+                continue;
+            }
+        }
+#endif
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
@@ -633,6 +654,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_MEGA_TIMES")) d->mega_times = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_SPREAD")) d->mega_spread = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_FILL")) d->mega_fill = std::atoi(e);
+    if (const char *e = std::getenv("RT_MEGA_TEAM")) d->mega_team = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -951,7 +973,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
-                               d->mega_shade_min | d->mega_trav_min << 8 | (lane_cap & 127) << 16,
+                               d->mega_shade_min | d->mega_trav_min << 8 | (lane_cap & 127) << 16 |
+                                   (d->mega_team ? 1 << 23 : 0),
                                same ? (const int *)d->order : nullptr, cost,
                                d->mega_times ? d->mega_tfin : nullptr);
             HIP_TRY(hipGetLastError());
@@ -972,9 +995,10 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyFromSymbolAsync(sg, HIP_SYMBOL(g_mega_seg), sizeof sg, 0, hipMemcpyDeviceToHost, stream));
                 HIP_TRY(hipStreamSynchronize(stream));
                 std::fprintf(stderr, "[mega prof] shade segments, cycles per shade iteration: mesh+emission=%.0f "
-                             "normal=%.0f mr=%.0f sample=%.0f pdf=%.0f base+brdf=%.0f\n",
+                             "normal=%.0f mr=%.0f sample=%.0f pdf=%.0f base+brdf=%.0f; team rays/wave=%.1f cyc/team ray=%.0f\n",
                              (double)sg[0] / pf[3], (double)sg[1] / pf[3], (double)sg[2] / pf[3],
-                             (double)sg[3] / pf[3], (double)sg[4] / pf[3], (double)sg[5] / pf[3]);
+                             (double)sg[3] / pf[3], (double)sg[4] / pf[3], (double)sg[5] / pf[3],
+                             (double)sg[7] / pf[7], sg[7] ? (double)sg[6] / sg[7] : 0.0);
             }
 #endif
             if (d->mega_times && count) {   // print finish-time percentiles (ms after the first finish) to stderr

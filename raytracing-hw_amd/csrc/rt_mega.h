@@ -18,6 +18,17 @@
 #pragma once
 #include "rt_wavefront.h"
 #include "rt_trav_wide.h"
+#include "rt_team.h"
+
+// RT_TEAM: a wave down to one traversing pixel walks that ray with all its lanes (rt_team.h).
+// Bit-exact (GPU parity tests), but measured on sponza 1080p x256spp: a team ray costs ~84 k
+// cycles against ~46 steps x 3-6 k cycles for a lane alone, yet the frame is no faster at 1
+// or 8 GPUs (a wave is rarely down to one pixel for long: the spread order puts pixels of
+// similar cost in every wave), and compiling the path in costs 7% (register allocation of
+// the main loop).  Off.
+#ifndef RT_TEAM
+#define RT_TEAM 0
+#endif
 
 // RT_WIDE: traversal by trav_step_w (rt_trav_wide.h: two node levels or two triangles per
 // iteration, from the wide node array) instead of trav_step (one unit per iteration).
@@ -133,6 +144,39 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
     }
     mega_sample<COUNT>(L, sc, g, root, cnt);
 }
+
+#if RT_TEAM && defined(__HIPCC__) && !RT_WIDE
+// The rest of lane `owner`'s ray by the whole wave (trav_team); false if its frames are not
+// all in LDS.  Then the owner is READY, as after its last trav_step.
+__device__ __forceinline__ bool mega_team(MegaLane &L, int owner, const DevScene &sc) {
+    const int lane = threadIdx.x & 63;
+    const int sp = (int)team_u((uint32_t)L.T.sp, owner);
+    if (sp > kLdsStack) return false;
+    Ray r;
+    r.o = V3{team_f(L.r.o.x, owner), team_f(L.r.o.y, owner), team_f(L.r.o.z, owner)};
+    r.d = V3{team_f(L.r.d.x, owner), team_f(L.r.d.y, owner), team_f(L.r.d.z, owner)};
+    r.inv = V3{team_f(L.r.inv.x, owner), team_f(L.r.inv.y, owner), team_f(L.r.inv.z, owner)};
+    TravState T;
+    T.a = team_u(L.T.a, owner);
+    T.b = team_u(L.T.b, owner);
+    T.k = team_u(L.T.k, owner);
+    T.kend = team_u(L.T.kend, owner);
+    T.acc = team_f(L.T.acc, owner);
+    T.sp = sp;
+    T.phase = (int)team_u((uint32_t)L.T.phase, owner);
+    T.best.t = team_f(L.T.best.t, owner);
+    T.best.u = team_f(L.T.best.u, owner);
+    T.best.v = team_f(L.T.best.v, owner);
+    T.best.prim = (int)team_u((uint32_t)L.T.best.prim, owner);
+    const TeamStack stk{(int)(threadIdx.x & ~63u), owner};
+    trav_team(sc, r, T, stk, lane);
+    if (lane == owner) {
+        L.T = T;
+        L.state = M_READY;
+    }
+    return true;
+}
+#endif
 
 // One iteration of a wave's main loop for one lane, given the wave's decision: shade the
 // READY lanes this iteration (shade_now), or step the traversing lanes.
