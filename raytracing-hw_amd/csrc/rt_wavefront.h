@@ -291,6 +291,15 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
 #ifndef RT_HOIST_LOADS
 #define RT_HOIST_LOADS 1
 #endif
+// trav_step_n keeps a far child's squared entry distance and compares it with the exact
+// midpoint test (sqrt_gt) instead of taking a correctly rounded sqrt per node step.  Exact
+// (tests/test_kernel_host.py), but 5% slower on sponza 1080p at 1 GPU (double-precision
+// compares on every return); off.  (Choosing the near child by selecting dir[split axis]
+// instead of the sign-bit mask was tried too: 1.6x slower — the register allocation of the
+// whole loop changed.)
+#ifndef RT_SQ_CULL
+#define RT_SQ_CULL 0
+#endif
 // Leaf triangles tested per trav_step (1-4; node arrays in plain memory only).  A node lane
 // and a leaf lane read through the same registers: 4 x 16 B of the child pair, or of
 // triangle k (its 3 x 16 B and the next record's first), then 3 x 16 B per further triangle.
@@ -355,6 +364,18 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
     return (bits & 8u) == 0;
 }
 
+// sqrtf(x) > a, correctly rounded sqrt, without the sqrt: for a > 0 with next float n,
+// sqrtf(x) > a iff sqrt(x) > (a + n) / 2 (a tie is impossible: (a + n)^2 / 4 is an odd
+// square of ulps, far wider than a float), i.e. 4x > (a + n)^2, both sides exact in double.
+// For a = +-0: sqrtf(x) > 0 iff x > 0.  NaN x: false, as the comparison it replaces.  x is a
+// squared length (>= 0 or NaN) and a a hit distance or the local best (>= 0, finite).
+__device__ __forceinline__ bool sqrt_gt(float x, float a) {
+    if (!(a > 0.f)) return x > 0.f;
+    const float n = __uint_as_float(__float_as_uint(a) + 1u);
+    const double m = (double)a + (double)n;
+    return 4.0 * (double)x > m * m;
+}
+
 // The return of trav_step: merge subtree bests upwards until a far child is to be visited
 // (enter it: false) or the stack is empty (T.best is final: true).
 template <class Stack>
@@ -373,7 +394,11 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
             acc = acc < p ? acc : p;
             continue;
         }
+#if RT_SQ_CULL
+        if (!sqrt_gt(__uint_as_float(f.y), acc)) {   // far child survives the near subtree's best
+#else
         if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
+#endif
             stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
 #ifdef RT_STACK_PROBE
             RT_STACK_PROBE(sp);
@@ -424,7 +449,15 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
         float cF[3];
         bool hL, hR, inF;
         box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
+#if RT_SQ_CULL
+        // the far child's squared entry distance (box_dist before its sqrt; 0 from inside)
+        const V3 dF = rtv::sub(V3{cF[0], cF[1], cF[2]}, r.o);
+        const float ef = inF ? 0.f : rtv::dot(dF, dF);
+        const bool ef_gt_1e9 = sqrt_gt(ef, 1e9f);
+#else
         const float ef = box_dist(cF, inF, r);
+        const bool ef_gt_1e9 = ef > 1e9f;
+#endif
         const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
         const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
         if (hn && hf) {
@@ -434,7 +467,7 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
             RT_STACK_PROBE(T.sp);
 #endif
         }
-        const bool far_only = !hn && hf && !(ef > 1e9f);
+        const bool far_only = !hn && hf && !ef_gt_1e9;
         if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
         else T.phase = TP_POP;
     } else if (at_leaf) {

@@ -349,3 +349,36 @@ extern "C" long long kh_box_pair_check(long long n, uint32_t seed) {
     }
     return bad;
 }
+
+// sqrt_gt(x, a) (rt_wavefront.h: the traversal's cull without the sqrt) against
+// sqrtf(x) > a, for squared lengths x and distances a >= 0: random pairs, x at and around
+// a^2 and around the squares of a's neighbours, special values.  Returns mismatches.
+extern "C" long long kh_sqrt_gt_check(long long n, uint32_t seed) {
+    uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto next = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+    auto bits = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
+    auto ubits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+    long long bad = 0;
+    auto check = [&](float x, float a) {
+        if (rtd::sqrt_gt(x, a) != (sqrtf(x) > a)) ++bad;
+    };
+    const float specials[] = {0.f, -0.f, 1e-45f, 1e-38f, 1e9f, 3.4e38f, __builtin_inff(), __builtin_nanf("")};
+    for (float x : specials)
+        for (float a : {0.f, -0.f, 1e-45f, 1e-20f, 1.f, 1e9f, 3e38f}) check(x, a);
+    for (long long k = 0; k < n; ++k) {
+        // a: any positive finite float (uniform in bits), or a typical distance
+        const uint64_t r = next();
+        float a = (r & 1) ? bits((uint32_t)(r >> 8) % 0x7f800000u) : (float)((r >> 16) & 0xffffff) / 65536.f;
+        const double a2 = (double)a * (double)a;
+        const float x0 = (float)a2;
+        // x around a^2 (a few ulps each way) and around the midpoint square
+        const float n1 = bits(ubits(a) + 1u);
+        const float mid2 = (float)(((double)a + (double)n1) * ((double)a + (double)n1) / 4.0);
+        for (int d = -3; d <= 3; ++d) {
+            if (x0 > 0.f) check(bits(ubits(x0) + (uint32_t)d), a);
+            if (mid2 > 0.f) check(bits(ubits(mid2) + (uint32_t)d), a);
+        }
+        check(bits((uint32_t)(next() >> 8) % 0x7f800000u), a);
+    }
+    return bad;
+}

@@ -40,6 +40,8 @@ def _build_kh(tmp_path_factory, *defines):
     lib.kh_render_mega.restype = I
     lib.kh_box_pair_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
     lib.kh_box_pair_check.restype = ctypes.c_int64
+    lib.kh_sqrt_gt_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
+    lib.kh_sqrt_gt_check.restype = ctypes.c_int64
     return lib
 
 
@@ -202,3 +204,10 @@ def test_box_pair_matches_single_box_test(kh):
     primitive.cpp:146-208, restated op for op) on 4 M random cases rich in special values:
     signed zeros, infinities, NaN, flat and inverted boxes, planes through the origin."""
     assert kh.kh_box_pair_check(4_000_000, 7) == 0
+
+
+def test_sqrt_gt_matches_sqrtf(kh):
+    """sqrt_gt (trav_step_n's far-child cull on the squared entry distance) equals
+    sqrtf(x) > a on 2 M distances, with x at and around a^2 and the midpoint square, and
+    special values; the traversal's decisions therefore stay the reference's."""
+    assert kh.kh_sqrt_gt_check(2_000_000, 11) == 0
