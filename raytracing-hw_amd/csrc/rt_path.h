@@ -394,11 +394,18 @@ __device__ __forceinline__ V4 tex_sample_ti(const DevScene &sc, const uint4 ti, 
     const int px = (int)floorf(p.x), py = (int)floorf(p.y);
     const float dx = p.x - floorf(p.x), dy = p.y - floorf(p.y);
     uint32_t texel[4];
+    // (px + d) % W without a division: p - floorf(p) is in [0, 1], so px is in [0, W] and
+    // px + d in [0, W + 1] <= 2W; two conditional subtractions give the remainder (W = 1
+    // included).  NaN coordinates convert to 0 on the device, as they would for %.
+    auto wrap = [](int v, int n) {
+        v = v >= n ? v - n : v;
+        return v >= n ? v - n : v;
+    };
 #pragma unroll
     for (int ddy = 0; ddy < 2; ++ddy)
 #pragma unroll
         for (int ddx = 0; ddx < 2; ++ddx) {
-            const int x = (px + ddx) % W, y = (py + ddy) % H;
+            const int x = wrap(px + ddx, W), y = wrap(py + ddy, H);
 #ifdef __HIPCC__
             // device copy: 4x4-texel tiles (rt_device.hip tile_textures)
             const uint32_t idx = (uint32_t)(((y >> 2) * ((W + 3) >> 2) + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3));
