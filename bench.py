@@ -101,7 +101,8 @@ def pmc_traffic(fetch_csv, write_csv, kernel_prefix):
     import csv
     def mean(path, counter):
         for row in csv.reader(open(path)):
-            if row and row[0].startswith(kernel_prefix) and row[1] == counter:
+            # the parity launch only (the fast-mode instantiation ends its template list in "true>")
+            if row and row[0].startswith(kernel_prefix) and "true>(" not in row[0] and row[1] == counter:
                 return float(row[4]) * 1024.0
         return None
     f, w = mean(fetch_csv, "FETCH_SIZE"), mean(write_csv, "WRITE_SIZE")
@@ -123,6 +124,9 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=1080, help="rows of the frame in the CPU baseline sample")
     ap.add_argument("--cpu-spp", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fast-steps", type=int, default=2,
+                    help="timed frames of fast mode (RT_FLAG_FAST, reported beside the headline; 0 = skip)")
+    ap.add_argument("--fast-chunk", type=int, default=16, help="fast mode: samples per work unit")
     ap.add_argument("--traffic-from", default="auto",
                     help="PMC summaries for roofline.traffic: a path prefix P (P_fetch*.csv / P_write*.csv from "
                          "tools/profile.sh of this same command), 'auto' (the committed profiles/ pair when the "
@@ -164,10 +168,11 @@ def main():
     frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(count=False):
+    def step(count=False, fast=False):
         # render the shard, finish it to 8 bits on the GPU (scene.cpp:54-64), gather the frame
         st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
-                                 count=count, kernel=args.kernel, stats=True, kernel_times=not count)
+                                 count=count, kernel=args.kernel, stats=True, kernel_times=not count, fast=fast,
+                                 fast_chunk=args.fast_chunk)
         rt.tonemap_device(out.data_ptr(), W, max_rows, S, rgb.data_ptr(), stream)
         rtdist.gather_frame(rgb, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
         return st
@@ -193,6 +198,32 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+
+    # fast mode (RT_FLAG_FAST): same frame, per-(pixel, sample) Philox streams, samples as
+    # independent work units; its own ray count (other random paths), same timing protocol
+    fast_line = None
+    if args.fast_steps > 0 and args.kernel == 0:
+        fc = step(count=True, fast=True)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        fast_ms = []
+        for _ in range(args.fast_steps):
+            fast_ms.append(step(fast=True)["render_ms"])
+        torch.cuda.synchronize()
+        barrier()
+        tf = torch.tensor([time.perf_counter() - tf, float(fc["rays"])], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(tf[0:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(tf[1:2], op=dist.ReduceOp.SUM)
+        fe, frays = float(tf[0].item()), float(tf[1].item())
+        fast_line = {"value": round(frays * args.fast_steps / fe / 1e6, 3), "unit": "Mrays/s",
+                     "ms_per_step": round(fe / args.fast_steps * 1e3, 3), "steps": args.fast_steps,
+                     "chunk": args.fast_chunk, "rays_per_frame": int(frays),
+                     "kernel_ms": round(float(np.mean(fast_ms)), 3),
+                     "note": "RT_FLAG_FAST: Philox4x32-10 seed per (pixel, sample), work units of `chunk` samples; "
+                             "statistically equivalent to the reference, NOT bit-identical (not the headline)"}
 
     keys = ["rays", "aabb_tests", "tri_tests", "light_queries", "light_aabb_tests", "light_tri_tests", "shading_hits"]
     local_counts = torch.tensor([counts[k] for k in keys], dtype=torch.float64, device="cuda")
@@ -266,6 +297,7 @@ def main():
                          "path_frame_bytes": int(bytes_frame), "path_frame_ms": round(frame_s * 1e3, 3),
                          "path_achieved": round(bytes_frame / frame_s / 1e9, 1)},
             "cpu_baseline": None,
+            "fast_mode": fast_line,
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)

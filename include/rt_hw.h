@@ -89,11 +89,18 @@ typedef struct {
     int32_t kernel;       /* 0 = lane-resident (default), 1 = one lane per pixel, 2 = persistent per-pixel,
                              3 = wave megakernel, 4 = wavefront (extend/shade launches) */
     int32_t flags;        /* RT_FLAG_* */
-    int32_t reserved;
+    int32_t fast_chunk;   /* RT_FLAG_FAST: samples per work unit (0 = 16)                 */
 } rt_params;
 
 /* rt_params.flags */
 #define RT_FLAG_KERNEL_TIMES 1  /* wavefront path (kernel 4): time every extend / shade launch (HIP events) */
+/* Fast mode (kernel 0 only): every (pixel, sample) draws from its own
+ * stream (Philox4x32-10 keyed by pixel j*W+i, counter = sample, seeds the sample's minstd
+ * stream; normal cache empty per sample), so a pixel's samples are independent work units
+ * of fast_chunk samples that any lane may run.  The pixel sum is the chunk partials added in
+ * chunk order: deterministic for a given fast_chunk, statistically equivalent to the
+ * reference, NOT bit-identical to it (the parity mode is the default). */
+#define RT_FLAG_FAST 2
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */

@@ -106,6 +106,34 @@ constexpr float kInvPiF = 0.318309886183790671538f;  // M_1_PIf32
 
 uint32_t ubits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 
+// Philox4x32-10: 10 rounds of two 32x32->64 multiplies (M0 = 0xD2511F53 on word 0,
+// M1 = 0xCD9E8D57 on word 2), output {hi1^c1^k0, lo1, hi0^c3^k1, lo0}; the key is bumped by
+// the Weyl constants (0x9E3779B9, 0xBB67AE85) before every round but the first.
+void philox4x32_10(const uint32_t *ctr, const uint32_t *key, uint32_t *out) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]}, k[2] = {key[0], key[1]};
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k[0] += 0x9E3779B9u;
+            k[1] += 0xBB67AE85u;
+        }
+        const uint64_t a = (uint64_t)0xD2511F53u * c[0], b = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(b >> 32) ^ c[1] ^ k[0], n2 = (uint32_t)(a >> 32) ^ c[3] ^ k[1];
+        c[0] = n0;
+        c[1] = (uint32_t)b;
+        c[2] = n2;
+        c[3] = (uint32_t)a;
+    }
+    for (int i = 0; i < 4; ++i) out[i] = c[i];
+}
+// Fast-mode seed of sample s of pixel pix: Philox word 0 (counter {s,0,0,0}, key {pix,
+// 0x5eed2026}), as minstd_rand's constructor takes it (it reduces mod 2^31-1, 0 -> 1).
+uint32_t philox_seed(uint32_t pix, uint32_t s) {
+    const uint32_t ctr[4] = {s, 0u, 0u, 0u}, key[2] = {pix, 0x5eed2026u};
+    uint32_t o[4];
+    philox4x32_10(ctr, key, o);
+    return o[0];
+}
+
 class Oracle {
 public:
     explicit Oracle(const rt_scene_view &v) : S(v) {}
@@ -476,6 +504,30 @@ public:
         normDist = nullptr;
         return sum;
     }
+    // Fast mode (include/rt_hw.h RT_FLAG_FAST; not the reference's RNG convention): sample s
+    // of pixel j*W+i runs minstd_rand seeded by philox_seed(j*W+i, s) with a fresh normal
+    // cache; samples summed per chunk of cs in order, chunk partials summed in chunk order.
+    Vec3 render_pixel_fast(int i, int j, int spp, int cs) const {
+        const uint32_t pix = (uint32_t)(j * S.width + i);
+        UniformF offset(-0.5f, 0.5f);
+        Vec3 total{0.f, 0.f, 0.f};
+        for (int c0 = 0; c0 < spp; c0 += cs) {
+            Vec3 part{0.f, 0.f, 0.f};
+            for (int s = c0; s < std::min(spp, c0 + cs); ++s) {
+                std::normal_distribution<float> nd(0.f, 1.f);
+                normDist = &nd;
+                Engine e(philox_seed(pix, (uint32_t)s));
+                float ox = offset(e);
+                float oy = offset(e);
+                Ray r = camera_ray(i, j, ox, oy);
+                r.power = S.ray_depth;
+                part += shade(r, e).color;
+            }
+            total += part;
+        }
+        normDist = nullptr;
+        return total;
+    }
 };
 thread_local Counts Oracle::cnt;
 thread_local std::normal_distribution<float> *Oracle::normDist = nullptr;
@@ -483,6 +535,29 @@ thread_local std::normal_distribution<float> *Oracle::normDist = nullptr;
 }  // namespace
 
 extern "C" {
+
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; Random123 philox.h constants): the fast
+// mode's per-sample seed source.  Pinned by Random123's known-answer vectors (test_oracle.py).
+void rt_oracle_philox(const uint32_t *ctr, const uint32_t *key, uint32_t *out) {
+    philox4x32_10(ctr, key, out);
+}
+
+// Fast-mode render of pixels [p0, p1) (see Oracle::render_pixel_fast); returns wall seconds.
+double rt_oracle_render_fast(const rt_scene_view *view, int spp, int chunk, int64_t p0, int64_t p1, int threads,
+                             float *out) {
+    Oracle o(*view);
+    const int W = view->width;
+    auto t0 = std::chrono::steady_clock::now();
+    int nt = threads > 0 ? threads : omp_get_max_threads();
+#pragma omp parallel for num_threads(nt) schedule(guided, 16)
+    for (int64_t p = p0; p < p1; ++p) {
+        Vec3 s = o.render_pixel_fast((int)(p % W), (int)(p / W), spp, chunk);
+        out[3 * (p - p0) + 0] = s.x;
+        out[3 * (p - p0) + 1] = s.y;
+        out[3 * (p - p0) + 2] = s.z;
+    }
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 
 // Renders pixels [p0, p1) of the row-major W*H frame (float RGB sums) with `threads`
 // OpenMP threads (0 = all).  counters (may be NULL): rays, aabb, tri, light queries,

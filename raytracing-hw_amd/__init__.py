@@ -46,12 +46,13 @@ class RtSceneView(ctypes.Structure):
 
 ABI_VERSION = 2          # include/rt_hw.h RT_ABI_VERSION
 FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES
+FLAG_FAST = 2            # RT_FLAG_FAST: per-(pixel, sample) Philox-seeded streams, not bit-identical to the reference
 
 
 class RtParams(ctypes.Structure):
     _fields_ = [("spp", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("row_block", ctypes.c_int32), ("count", ctypes.c_int32), ("kernel", ctypes.c_int32),
-                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("fast_chunk", ctypes.c_int32)]
 
 
 class RtStats(ctypes.Structure):
@@ -203,24 +204,29 @@ class Scene:
     def upload(self, device=0):
         _check(lib().rt_scene_upload(self._h, device))
 
-    def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False):
-        return RtParams(spp or 0, rank, world, row_block, int(count), kernel, FLAG_KERNEL_TIMES if kernel_times else 0)
+    def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False, fast=False, fast_chunk=0):
+        flags = (FLAG_KERNEL_TIMES if kernel_times else 0) | (FLAG_FAST if fast else 0)
+        return RtParams(spp or 0, rank, world, row_block, int(count), kernel, flags, fast_chunk)
 
-    def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0):
-        """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42)."""
+    def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0, fast=False,
+                    fast_chunk=0):
+        """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42).
+        fast=True: fast mode (RT_FLAG_FAST, work units of fast_chunk samples): statistically
+        equivalent to the reference, not bit-identical."""
         self.upload(device)
         rows = shard_rows(self.height, rank, world, row_block)
         out = np.zeros((len(rows), self.width, 3), np.float32)
         st = RtStats()
-        p = self._params(spp, rank, world, row_block, count, kernel)
+        p = self._params(spp, rank, world, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk)
         _check(lib().rt_render(self._h, ctypes.byref(p), out.ctypes.data_as(_c_f), ctypes.byref(st)))
         return out, st.as_dict()
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
-                      kernel=0, stats=False, kernel_times=False):
+                      kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0):
         """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream.
-        kernel_times: per-launch HIP-event timing of the wavefront kernels (needs stats)."""
-        p = self._params(spp, rank, world, row_block, count, kernel, kernel_times)
+        kernel_times: per-launch HIP-event timing of the wavefront kernels (needs stats).
+        fast: fast mode (RT_FLAG_FAST), see render_sums."""
+        p = self._params(spp, rank, world, row_block, count, kernel, kernel_times, fast, fast_chunk)
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))

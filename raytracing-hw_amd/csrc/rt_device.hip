@@ -71,6 +71,8 @@ struct rt_device_scene {
     int mega_fill = 0;                 // RT_MEGA_FILL: fewer pixels than lanes -> every resident wave, fewer lanes each
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
+    float *fast_part = nullptr;        // fast mode: chunk-major partial sums (chunks x pixels x 3)
+    long long fast_part_cap = 0;       // floats
     // that order (per shard geometry): pixel indices by descending traversal work
     int *order = nullptr;
     unsigned *order_cost = nullptr;
@@ -229,11 +231,15 @@ __global__ void __launch_bounds__(256) rt_finish_kernel(const float *sum, long l
 __device__ unsigned long long g_mega_prof[8];
 __device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT_PROF_SEG)
 #endif
-template <bool COUNT, int WPE>
+// FAST (RT_FLAG_FAST): queue items are (chunk, pixel) work units of
+// `cs` samples with per-sample Philox seeds; `out` is then the chunk-major partial buffer
+// that rt_fast_reduce_kernel folds.
+template <bool COUNT, int WPE, bool FAST = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
                                                        int shade_min, const int *order, unsigned *cost,
-                                                       unsigned long long *tfin) {
+                                                       unsigned long long *tfin, int cs = 0) {
+    const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels;
     const int lane = threadIdx.x & 63;
     // texel-decode LUT in LDS: the shading's lane-dependent lookups become ds_reads
     __shared__ float lut[512];
@@ -276,9 +282,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                 base = __shfl(base, leader, 64);
                 if (need) {
                     const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (p < g.n_pixels) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : p, root, cnt);
+                    if (p < n_items) {
+                        if (FAST) rtd::mega_assign_fast<COUNT>(L, sc, g, p, cs, spp, root, cnt);
+                        else rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : p, root, cnt);
+                    }
                 }
-                if ((long long)base + cm >= g.n_pixels) exhausted = true;
+                if ((long long)base + cm >= n_items) exhausted = true;
 
             }
         }
@@ -316,7 +325,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
             pf[shade_now ? 5 : 6] += (unsigned long long)(shade_now ? nr : nt);
         }
 #endif
-        if (COUNT && tfin) {   // diagnostics (RT_MEGA_TIMES, counting renders only)
+        if (FAST) {
+            rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), true>(L, shade_now, sc, g, st, spp, out, cost, root,
+                                                                         S, nodes, cnt);
+        } else if (COUNT && tfin) {   // diagnostics (RT_MEGA_TIMES, counting renders only)
             const long long pix_before = L.pix;
             rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
             if (pix_before >= 0 && L.pix < 0) tfin[pix_before] = wall_clock64();
@@ -340,6 +352,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
 #endif
     flush_counters<COUNT>(cnt, counters);
+}
+
+// Fast mode: pixel sum = partials of chunks 0, 1, ... added in order (deterministic; the
+// oracle's rt_oracle_render_fast adds them the same way).  part is chunk-major: n3 floats
+// per chunk.
+__global__ void __launch_bounds__(256) rt_fast_reduce_kernel(const float *__restrict__ part, float *__restrict__ out,
+                                                             long long n3, int chunks) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n3) return;
+    float s = 0.f;
+    for (int c = 0; c < chunks; ++c) s += part[(long long)c * n3 + i];
+    out[i] = s;
 }
 
 // ------------------------------------------------------------------------ wavefront
@@ -865,6 +889,9 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
     const int world = p->world > 0 ? p->world : 1, rank = p->rank, rb = p->row_block > 0 ? p->row_block : 8;
     const int spp = p->spp > 0 ? p->spp : s->samples;
     if (spp < 1) return rt_fail(RT_ERR_ARG, "rt_render: samples per pixel must be >= 1");
+    if ((p->flags & RT_FLAG_FAST) && p->kernel != 0)
+        return rt_fail(RT_ERR_ARG, "rt_render: fast mode (RT_FLAG_FAST) runs on kernel 0 only");
+    if (p->fast_chunk < 0) return rt_fail(RT_ERR_ARG, "rt_render: fast_chunk must be >= 0");
     const int64_t rows = rt_shard_rows_impl(s->height, rank, world, rb, nullptr);
     if (rows < 0) return RT_ERR_ARG;
     ShardGeom g{s->width, rank, world, rb, (long long)rows * s->width};
@@ -898,7 +925,15 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (rc) return rc;
         } else if (p->kernel == 0) {   // lane-resident (rt_mega.h), the default
             if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "ray_depth must be in [1, 15]");
+            // fast mode (RT_FLAG_FAST): work units of `cs` samples, Philox seed per sample
+            const bool fast = (p->flags & RT_FLAG_FAST) != 0;
+            const int cs = fast ? std::min(spp, p->fast_chunk > 0 ? p->fast_chunk : 16) : 0;
+            const int chunks = fast ? (spp + cs - 1) / cs : 1;
+            const long long n_items = g.n_pixels * chunks;
+            if (fast && n_items > (long long)UINT32_MAX - 65536)
+                return rt_fail(RT_ERR_LIMIT, "rt_render: fast mode work units exceed the 32-bit queue");
             auto pick = [&](int wpe) {
+                if (fast) return count ? rt_mega_kernel<true, 5, true> : rt_mega_kernel<false, 5, true>;
                 switch (wpe) {
                     case 5: return count ? rt_mega_kernel<true, 5> : rt_mega_kernel<false, 5>;
                     case 6: return count ? rt_mega_kernel<true, 6> : rt_mega_kernel<false, 6>;
@@ -911,13 +946,13 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mk, 256, 0));
             if (per_cu < 1) per_cu = 1;
             if (d->mega_occ > 0) per_cu = std::min(per_cu, d->mega_occ);
-            const long long need = (g.n_pixels + 255) / 256, resident = (long long)d->cu_count * per_cu;
+            const long long need = (n_items + 255) / 256, resident = (long long)d->cu_count * per_cu;
             unsigned blocks = (unsigned)std::min<long long>(need, resident);
             if (blocks == 0) blocks = 1;
             // RT_MEGA_FILL: with fewer pixels than resident lanes, launch every resident wave and
             // give each ceil(pixels / waves) lanes: more, narrower waves per SIMD
             int lane_cap = 64;
-            if (d->mega_fill && need < resident) {
+            if (d->mega_fill && need < resident && !fast) {
                 blocks = (unsigned)resident;
                 lane_cap = (int)std::min<long long>(64, (g.n_pixels + 4LL * blocks - 1) / (4LL * blocks));
             }
@@ -937,7 +972,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             //     back).  Rank-0 shard of an 8-way split: 490 -> 353 ms; 1 GPU: +1-2%.
             //     Plain heaviest-first (RT_MEGA_SPREAD=0) only with >= RT_MEGA_ORDER_MIN pixels
             //     per lane: with fewer it clusters the heavy pixels in the same waves.
-            const bool many = g.n_pixels >= (long long)d->mega_order_min * blocks * 256 || d->mega_spread;
+            const bool many = !fast && (g.n_pixels >= (long long)d->mega_order_min * blocks * 256 || d->mega_spread);
             const bool same = many && d->order && d->order_n == g.n_pixels && d->order_key[0] == rank &&
                               d->order_key[1] == world && d->order_key[2] == rb && d->order_valid && d->mega_reorder;
             unsigned *cost = nullptr;
@@ -945,7 +980,6 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 if (d->order_cap < g.n_pixels) {
                     if (d->order) (void)hipFree(d->order);
                     if (d->order_cost) (void)hipFree(d->order_cost);
-        if (d->mega_tfin) (void)hipFree(d->mega_tfin);
                     d->order = nullptr;
                     d->order_cost = nullptr;
                     d->order_cap = 0;
@@ -954,6 +988,17 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                     d->order_cap = g.n_pixels;
                 }
                 cost = d->order_cost;
+            }
+            float *k_out = d_out;
+            if (fast) {
+                if (d->fast_part_cap < n_items * 3) {
+                    if (d->fast_part) (void)hipFree(d->fast_part);
+                    d->fast_part = nullptr;
+                    d->fast_part_cap = 0;
+                    HIP_TRY(hipMalloc((void **)&d->fast_part, sizeof(float) * n_items * 3));
+                    d->fast_part_cap = n_items * 3;
+                }
+                k_out = d->fast_part;
             }
             if (d->mega_times && d->mega_tfin_n < g.n_pixels) {   // RT_MEGA_TIMES: per-pixel finish clocks
                 if (d->mega_tfin) (void)hipFree(d->mega_tfin);
@@ -972,12 +1017,18 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
             }
 #endif
-            hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, d_out, d->counters, d->queue,
+            hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
                                d->mega_shade_min | d->mega_trav_min << 8 | (lane_cap & 127) << 16 |
                                    (d->mega_team ? 1 << 23 : 0),
                                same ? (const int *)d->order : nullptr, cost,
-                               d->mega_times ? d->mega_tfin : nullptr);
+                               d->mega_times && !fast ? d->mega_tfin : nullptr, cs);
             HIP_TRY(hipGetLastError());
+            if (fast) {
+                const long long n3 = g.n_pixels * 3;
+                hipLaunchKernelGGL(rt_fast_reduce_kernel, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, stream,
+                                   (const float *)d->fast_part, d_out, n3, chunks);
+                HIP_TRY(hipGetLastError());
+            }
 #ifdef RT_MEGA_PROF
             {
                 unsigned long long pf[8];
@@ -1121,6 +1172,7 @@ void rt_device_scene_release(rt_scene *s) {
         if (d->order) (void)hipFree(d->order);
         if (d->order_cost) (void)hipFree(d->order_cost);
         if (d->mega_tfin) (void)hipFree(d->mega_tfin);
+        if (d->fast_part) (void)hipFree(d->fast_part);
         if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
         for (hipStream_t &x : d->wf_stream)
             if (x) (void)hipStreamDestroy(x);

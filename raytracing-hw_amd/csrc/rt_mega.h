@@ -68,6 +68,12 @@ enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2 };
 struct MegaLane {
     long long pix;   // shard pixel (slot), -1 = none
     int s, power, nv, state;
+    // fast mode only (RT_FLAG_FAST): work unit = samples [s, send) of the pixel; its partial
+    // sum goes to dst; gpix = j*W+i keys the per-sample Philox seed.  Unused fields of the
+    // parity kernel are dropped by the compiler.
+    int send;
+    uint32_t gpix;
+    long long dst;
     unsigned long long work0;   // counting runs: traversal tests before this pixel (pixel cost)
     Rng rng;
     V3 sum;
@@ -88,10 +94,12 @@ __device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Cou
 #endif
 }
 
-// Next sample of the lane's pixel: jittered camera ray (scene.cpp:36-39).
-template <bool COUNT>
+// Next sample of the lane's pixel: jittered camera ray (scene.cpp:36-39).  Fast mode: the
+// sample's own Philox-seeded stream (rt_path.h fast_sample_seed).
+template <bool COUNT, bool FAST = false>
 __device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
                                             Counters &cnt) {
+    if (FAST) L.rng = Rng{fast_sample_seed(L.gpix, (uint32_t)L.s), 0u, 0.f};
     L.r = start_sample(sc, g, L.pix, L.rng, L.power);
     L.nv = 0;
     mega_begin<COUNT>(L, root, cnt);
@@ -111,9 +119,26 @@ __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, con
     mega_sample<COUNT>(L, sc, g, root, cnt);
 }
 
+// Fast mode: queue item q = chunk * n_pixels + pixel (every pixel's first chunk, then the
+// second, ...: neighbouring lanes take neighbouring pixels); samples [chunk*cs, +cs) of the
+// pixel, partial sum to slot q of the chunk-major partial buffer.
+template <bool COUNT>
+__device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc, const ShardGeom &g, long long q,
+                                                 int cs, int spp, const NodeRec &root, Counters &cnt) {
+    const long long c = q / g.n_pixels, p = q - c * g.n_pixels;
+    L.pix = p;
+    L.dst = q;
+    L.s = (int)c * cs;
+    L.send = L.s + cs < spp ? L.s + cs : spp;
+    L.sum = V3{0.f, 0.f, 0.f};
+    const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
+    L.gpix = (uint32_t)(py * sc.width + px);
+    mega_sample<COUNT, true>(L, sc, g, root, cnt);
+}
+
 // Shade the lane's closest hit (one vertex of scene.cpp:85-154); bounce, or end the path:
 // fold, accumulate, next sample or pixel done.
-template <bool COUNT>
+template <bool COUNT, bool FAST = false>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Counters &cnt) {
 #if RT_LANE_RECORDS
@@ -133,16 +158,17 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
         return;
     }
     L.sum = rtv::add(L.sum, fold_path(P, L.nv));
-    if (++L.s == spp) {
-        out[3 * L.pix + 0] = L.sum.x;
-        out[3 * L.pix + 1] = L.sum.y;
-        out[3 * L.pix + 2] = L.sum.z;
-        if (COUNT && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
+    if (++L.s == (FAST ? L.send : spp)) {
+        const long long o = FAST ? L.dst : L.pix;
+        out[3 * o + 0] = L.sum.x;
+        out[3 * o + 1] = L.sum.y;
+        out[3 * o + 2] = L.sum.z;
+        if (COUNT && !FAST && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
         L.pix = -1;
         L.state = M_IDLE;
         return;
     }
-    mega_sample<COUNT>(L, sc, g, root, cnt);
+    mega_sample<COUNT, FAST>(L, sc, g, root, cnt);
 }
 
 #if RT_TEAM && defined(__HIPCC__) && !RT_WIDE
@@ -180,12 +206,12 @@ __device__ __forceinline__ bool mega_team(MegaLane &L, int owner, const DevScene
 
 // One iteration of a wave's main loop for one lane, given the wave's decision: shade the
 // READY lanes this iteration (shade_now), or step the traversing lanes.
-template <bool COUNT, class Stack, class Nodes>
+template <bool COUNT, class Stack, class Nodes, bool FAST = false>
 __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
                                              const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt) {
     if (shade_now) {
-        if (L.state == M_READY) mega_shade<COUNT>(L, sc, g, st, spp, out, cost, root, cnt);
+        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, cnt);
     } else if (L.state == M_TRAV) {
 #if RT_WIDE
         if (trav_step_w<COUNT>(sc, L.r, L.T, stk, cnt)) L.state = M_READY;

@@ -14,11 +14,13 @@
 #include <cmath>
 #include <cstring>
 #define __device__
+#define __host__
 #define __forceinline__ inline
 struct float4 { float x, y, z, w; };
 struct uint2 { uint32_t x, y; };
 struct uint4 { uint32_t x, y, z, w; };
 inline uint2 make_uint2(uint32_t a, uint32_t b) { return {a, b}; }
+inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return {a, b, c, d}; }
 inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 inline int __float_as_int(float f) { int u; std::memcpy(&u, &f, 4); return u; }
@@ -122,6 +124,30 @@ struct Rng {
     uint32_t saved_avail;
     float saved;
 };
+
+// Fast mode (RT_FLAG_FAST): every (pixel, sample) gets its own stream, so
+// a pixel's samples no longer form one sequential chain and can run on any lane in any
+// order.  Philox4x32-10 (Salmon et al., SC'11; Random123's constants and round function),
+// counter = {sample, 0, 0, 0}, key = {pixel index j*W+i, kFastKey}, word 0 seeds the
+// sample's minstd stream the way minstd_rand(seed) does (mod 2^31-1, 0 -> 1); the polar
+// normal cache starts empty at every sample.  Draw order and arithmetic inside a sample
+// are the parity path's.  Statistically equivalent to the reference, not bit-identical.
+constexpr uint32_t kFastKey = 0x5eed2026u;
+__host__ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k.x += 0x9E3779B9u;
+            k.y += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y, (uint32_t)p0);
+    }
+    return c;
+}
+__host__ __device__ __forceinline__ uint32_t fast_sample_seed(uint32_t pixel, uint32_t sample) {
+    const uint32_t w = philox4x32_10(make_uint4(sample, 0u, 0u, 0u), make_uint2(pixel, kFastKey)).x % 2147483647u;
+    return w == 0 ? 1u : w;
+}
 
 __device__ __forceinline__ uint32_t rng_next(Rng &r) {
     uint64_t t = (uint64_t)r.x * 48271u;                          // < 2^47

@@ -120,6 +120,11 @@ class Oracle:
         V = ctypes.c_void_p
         self.lib.rt_oracle_render.restype = ctypes.c_double
         self.lib.rt_oracle_render.argtypes = [V, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, V, V]
+        self.lib.rt_oracle_render_fast.restype = ctypes.c_double
+        self.lib.rt_oracle_render_fast.argtypes = [V, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                                   ctypes.c_int, V]
+        self.lib.rt_oracle_philox.restype = None
+        self.lib.rt_oracle_philox.argtypes = [V, V, V]
         self.lib.rt_oracle_rays.restype = None
         self.lib.rt_oracle_rays.argtypes = [V, ctypes.c_int64, V, V, V, V]
 
@@ -133,6 +138,24 @@ class Oracle:
         secs = self.lib.rt_oracle_render(ctypes.addressof(v), spp, p0, p1, threads, out.ctypes.data, cnt.ctypes.data)
         del keep
         return out, cnt, secs
+
+    def render_fast(self, arrays, spp, chunk, p0=0, p1=None, threads=0):
+        """Fast mode (RT_FLAG_FAST) restated: per-sample Philox seeds, chunk partials."""
+        rt = package()
+        v, keep = rt.make_view(arrays)
+        W, H = int(arrays["width"]), int(arrays["height"])
+        p1 = W * H if p1 is None else p1
+        out = np.zeros((p1 - p0, 3), np.float32)
+        secs = self.lib.rt_oracle_render_fast(ctypes.addressof(v), spp, chunk, p0, p1, threads, out.ctypes.data)
+        del keep
+        return out, secs
+
+    def philox(self, ctr, key):
+        c = np.ascontiguousarray(ctr, np.uint32)
+        k = np.ascontiguousarray(key, np.uint32)
+        o = np.zeros(4, np.uint32)
+        self.lib.rt_oracle_philox(c.ctypes.data, k.ctypes.data, o.ctypes.data)
+        return o
 
     def rays(self, arrays, org, dirs):
         rt = package()
