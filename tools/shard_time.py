@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--kernels", default="0")
+    ap.add_argument("--chunks", default="0", help="0 = parity mode; k > 0 = fast mode (RT_FLAG_FAST) with k-sample units")
     args = ap.parse_args()
     rt = bench.import_pkg()
     scenes = bench.load_scenes_module()
@@ -42,20 +43,23 @@ def main():
     rtdist = __import__("importlib").import_module("raytracing_hw_amd.dist")
     stream = torch.cuda.current_stream().cuda_stream
     base = None
-    for kernel in [int(x) for x in args.kernels.split(",")]:
+    modes = [(k, c) for k in [int(x) for x in args.kernels.split(",")] for c in [int(x) for x in args.chunks.split(",")]]
+    for kernel, chunk in modes:
+        base = None
+        kw = dict(fast=chunk > 0, fast_chunk=max(chunk, 0))
         for world in [int(x) for x in args.worlds.split(",")]:
             rows = rtdist.max_shard_rows(H, world)
             out = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda")
             st = scene.render_device(out.data_ptr(), stream, spp=S, rank=0, world=world, count=True, stats=True,
-                                     kernel=kernel)
+                                     kernel=kernel, **kw)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                scene.render_device(out.data_ptr(), stream, spp=S, rank=0, world=world, stats=True, kernel=kernel)
+                scene.render_device(out.data_ptr(), stream, spp=S, rank=0, world=world, stats=True, kernel=kernel, **kw)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / args.steps * 1e3
             base = base or ms
-            print(json.dumps({"kernel": kernel, "world": world, "rank0_ms": round(ms, 2), "rank0_rays": st["rays"],
+            print(json.dumps({"kernel": kernel, "fast_chunk": chunk, "world": world, "rank0_ms": round(ms, 2), "rank0_rays": st["rays"],
                               "rank0_mrays_s": round(st["rays"] / ms / 1e3, 1),
                               "est_speedup_vs_1": round(base / ms, 2)}), flush=True)
 
