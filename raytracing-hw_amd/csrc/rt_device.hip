@@ -69,6 +69,12 @@ struct rt_device_scene {
     int mega_spread = 1;               // RT_MEGA_SPREAD: first pixels of a wave's lanes from different cost strata
     int mega_team = 1;                 // RT_MEGA_TEAM (builds with RT_TEAM=1): a wave's last traversing pixel walked by all its lanes
     int mega_fill = 0;                 // RT_MEGA_FILL: fewer pixels than lanes -> every resident wave, fewer lanes each
+    // RT_LIGHT_SPLIT_MIN: light-split kernel (rt_mega.h light_step) from this many emissive
+    // triangles (0 = never, the default).  Bit-exact, but measured slower on practice6_1
+    // (1,152 lights): -20% at 256x256x4, -13% at 1024x1024x4, -4% at 1920x1080x16
+    // (profiles/r01b_light_split_ab.jsonl): the two shading passes per vertex and the walk's
+    // extra main-loop iterations cost more than the lockstep walk inside the shading batch.
+    int light_split_min = 0;
     unsigned long long *mega_tfin = nullptr;
     long long mega_tfin_n = 0;
     float *fast_part = nullptr;        // fast mode: chunk-major partial sums (chunks x pixels x 3)
@@ -234,7 +240,13 @@ __device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT
 // FAST (RT_FLAG_FAST): queue items are (chunk, pixel) work units of
 // `cs` samples with per-sample Philox seeds; `out` is then the chunk-major partial buffer
 // that rt_fast_reduce_kernel folds.
-template <bool COUNT, int WPE, bool FAST = false>
+// RT_MEGA_NODE_LDS: traversal reads the top BVH levels from LDS (A/B knob, off)
+#ifndef RT_MEGA_NODE_LDS
+#define RT_MEGA_NODE_LDS 0
+#endif
+// LSPLIT: the light pdf's light-BVH walk as a lane state (rt_mega.h light_step), for scenes
+// with many emissive triangles (RT_LIGHT_SPLIT_MIN).
+template <bool COUNT, int WPE, bool FAST = false, bool LSPLIT = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out,
                                                        unsigned long long *counters, unsigned int *queue,
                                                        int shade_min, const int *order, unsigned *cost,
@@ -255,7 +267,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
 #else
     rtd::LdsStack S{spill};
 #endif
+#if RT_MEGA_NODE_LDS
+    // top kLdsNodes nodes of the breadth-first node array in LDS (rt_wavefront.h LdsNodes)
+    const rtd::LdsNodes nodes{sc.node};
+    rtd::LdsNodes::fill(sc.node, sc.n_nodes);
+#else
     const rtd::GlobalNodes nodes{sc.node};
+#endif
     const rtd::NodeRec root = rtd::load_node(rtd::mega_nodes(sc), 0);
     rtd::MegaLane L;
     L.pix = -1;
@@ -292,8 +310,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
             }
         }
         if (!__any(L.pix >= 0)) break;
-        const int nr = __popcll(__ballot(L.state == rtd::M_READY));
-        const int nt = __popcll(__ballot(L.state == rtd::M_TRAV));
+        const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
+        const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
         // shade_min: low byte = ready lanes that trigger a shading pass; next byte = shade
         // anyway once no more than this many lanes are still traversing
         const bool shade_now = nr > 0 && (nr >= (shade_min & 255) || nt <= ((shade_min >> 8) & 255));
@@ -325,9 +343,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
             pf[shade_now ? 5 : 6] += (unsigned long long)(shade_now ? nr : nt);
         }
 #endif
-        if (FAST) {
-            rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), true>(L, shade_now, sc, g, st, spp, out, cost, root,
-                                                                         S, nodes, cnt);
+        if (FAST || LSPLIT) {
+            rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
+                                                                               root, S, nodes, cnt);
         } else if (COUNT && tfin) {   // diagnostics (RT_MEGA_TIMES, counting renders only)
             const long long pix_before = L.pix;
             rtd::mega_iterate<COUNT>(L, shade_now, sc, g, st, spp, out, cost, root, S, nodes, cnt);
@@ -679,6 +697,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     if (const char *e = std::getenv("RT_MEGA_SPREAD")) d->mega_spread = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_FILL")) d->mega_fill = std::atoi(e);
     if (const char *e = std::getenv("RT_MEGA_TEAM")) d->mega_team = std::atoi(e);
+    if (const char *e = std::getenv("RT_LIGHT_SPLIT_MIN")) d->light_split_min = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_WF_NODE_COST")) d->wf_node_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_LEAF_COST")) d->wf_leaf_cost = std::atoi(e);
     if (const char *e = std::getenv("RT_WF_GROUPS")) d->wf_groups = std::max(1, std::min(kMaxGroups, std::atoi(e)));
@@ -723,7 +742,7 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     d->wf_count = nullptr;
     d->wf_host_count = nullptr;
     const long long cap = ((n + 255) / 256) * 256;
-    const int planes = 8 + 9 * D              // slot state (2 x 16 B), vertex records (36 B each)
+    const int planes = 8 + 9 * D + 20         // slot state (2 x 16 B), vertex records (36 B each), light-split mid (80 B)
                        + 2 * 4 * rtd::kQRec + 4;   // two ray queues (48 B / entry), hits (16 B / entry)
     const size_t bytes = (size_t)cap * 4 * (size_t)planes;
     HIP_TRY(hipMalloc(&d->wf_buf, bytes));
@@ -745,6 +764,7 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     w.st = (float4 *)take(8);
     w.rec_ab = (float4 *)take(8 * D);
     w.rec_c = take(D);
+    w.mid = (float4 *)take(20);   // 5 planes of float4, stride = lane slots (<= cap)
     d->wf_cap = cap;
     d->wf_D = D;
     return RT_OK;
@@ -932,8 +952,11 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const long long n_items = g.n_pixels * chunks;
             if (fast && n_items > (long long)UINT32_MAX - 65536)
                 return rt_fail(RT_ERR_LIMIT, "rt_render: fast mode work units exceed the 32-bit queue");
+            // light-split kernel for scenes with many emissive triangles (parity mode)
+            const bool lsplit = !fast && d->ds.n_lights >= d->light_split_min && d->light_split_min > 0;
             auto pick = [&](int wpe) {
                 if (fast) return count ? rt_mega_kernel<true, 5, true> : rt_mega_kernel<false, 5, true>;
+                if (lsplit) return count ? rt_mega_kernel<true, 5, false, true> : rt_mega_kernel<false, 5, false, true>;
                 switch (wpe) {
                     case 5: return count ? rt_mega_kernel<true, 5> : rt_mega_kernel<false, 5>;
                     case 6: return count ? rt_mega_kernel<true, 6> : rt_mega_kernel<false, 6>;

@@ -63,7 +63,8 @@ using MegaTrav = TravState;
 __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return sc.node; }
 #endif
 
-enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2 };
+// M_LTRAV / M_LREADY: light-pdf walk as its own traversal (light-split kernel, below)
+enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4 };
 
 struct MegaLane {
     long long pix;   // shard pixel (slot), -1 = none
@@ -171,6 +172,125 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
     mega_sample<COUNT, FAST>(L, sc, g, root, cnt);
 }
 
+// ---------------------------------------------------------------- light-split kernel
+// ManyLightsDistribution::pdf (random.cpp:179-188) walks the light BVH
+// with BVH::intersectAll (bvh.cpp:245-279) at every shading event.  With many emissive
+// triangles (C1: 1,152, 21.5 box + 11.5 triangle tests per walk) that walk is a second
+// traversal; inline in the shading batch it runs with the batch's lanes in lockstep and
+// holds the wave until the longest walk ends.  The light-split kernel runs it as a lane
+// state instead: shade_pre, then M_LTRAV (one light-BVH node per iteration, interleaved with
+// other lanes' scene traversal), then M_LREADY and shade_post in a later shading batch.
+// The shading state that crosses the walk is a lane-slot record (WfState::mid, 5 planes of
+// float4): (pos, r2) (N, metallic) (dir, mesh) (incoming dir, tc.x) (tc.y).  The walk reuses
+// the lane's traversal stack (empty once its closest hit is known) and TravState: sp, and
+// acc as the pdf sum.  Same operations in the same order as light_pdf, so the same bits.
+
+// One node of the walk: pop; a leaf sums its triangles' pdf terms in index order, an
+// internal node pushes the children whose boxes the ray hits (right, then left: left is
+// visited first).  `dir_rec` holds the un-normalized sample direction (light_pdf's
+// `direction`).  Returns true when the stack is empty.
+template <bool COUNT, class Stack>
+__device__ __forceinline__ bool light_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, Counters &cnt,
+                                           const float4 *dir_rec) {
+    const uint32_t id = stk.get(--T.sp).x;
+    const NodeRec nd = load_node(sc.light_node, id);
+    if ((nd.b & 3u) == 3u) {
+        const uint32_t first = nd.a, count = nd.b >> 2;
+        for (uint32_t k = first; k < first + count; ++k) {
+            const float4 a = sc.light[4 * k], b = sc.light[4 * k + 1], c = sc.light[4 * k + 2], w = sc.light[4 * k + 3];
+            TriHit h;
+            if (COUNT) cnt.ltri++;
+            if (tri_hit(V3{a.x, a.y, a.z}, V3{a.w, b.x, b.y}, V3{b.z, b.w, c.x}, r, h)) {
+                V3 n{c.y, c.z, c.w};
+                if (rtv::dot(r.d, n) > 0) n = rtv::neg(n);
+                const float4 dq = *dir_rec;
+                const float probability = 1.f / w.x;   // 1 / triangle_area (random.cpp:88)
+                T.acc += fabsf(probability * (h.t * h.t) / rtv::dot(n, V3{dq.x, dq.y, dq.z}));
+            }
+        }
+    } else {
+        const uint32_t left = nd.a;
+        float e;
+        const NodeRec l = load_node(sc.light_node, left), rr = load_node(sc.light_node, left + 1);
+        if (COUNT) cnt.laabb += 2;
+        const bool hl = aabb_hit(l.mn, l.mx, r, e);
+        const bool hr = aabb_hit(rr.mn, rr.mx, r, e);
+        RT_CHECK(T.sp + 2 <= kStack, 13, T.sp, T.sp = 0);
+        if (hr) stk.put(T.sp++, make_uint2(left + 1, 0u));
+        if (hl) stk.put(T.sp++, make_uint2(left, 0u));
+    }
+    return T.sp == 0;
+}
+
+// Shading of the light-split kernel: a READY lane runs shade_pre and starts its light walk
+// (or, without lights, finishes the vertex); an LREADY lane finishes the vertex with the
+// walked pdf.  The rest is mega_shade's: bounce, or fold and next sample / pixel.
+template <bool COUNT, bool FAST, class Stack>
+__device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc, const ShardGeom &g,
+                                                 const WfState &st, int spp, float *out, unsigned *cost,
+                                                 const NodeRec &root, Stack &stk, Counters &cnt) {
+    const long long slot = mega_slot();
+    LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, slot, st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
+    float4 *mid = st.mid + slot;
+    const long long ln = st.lanes;
+    bool next = false;
+    if (L.state == M_READY) {
+        const Hit h = L.T.best;
+        ShadeMid m;
+        if (h.prim >= 0 && h.t < sc.max_distance && shade_pre<COUNT>(sc, L.r, h, L.rng, cnt, P, L.nv, m)) {
+            if (sc.n_lights) {
+                P.flush_e();
+                mid[0] = make_float4(m.pos.x, m.pos.y, m.pos.z, m.r2);
+                mid[ln] = make_float4(m.N.x, m.N.y, m.N.z, m.metallic);
+                mid[2 * ln] = make_float4(m.dir.x, m.dir.y, m.dir.z, __int_as_float(m.mesh));
+                mid[3 * ln] = make_float4(L.r.d.x, L.r.d.y, L.r.d.z, m.tc.x);
+                mid[4 * ln] = make_float4(m.tc.y, 0.f, 0.f, 0.f);
+                if (COUNT) cnt.lq++;
+                L.r = make_ray(m.pos, m.dir);   // light_pdf's Ray(point, direction)
+                L.T.acc = 0.f;
+                L.T.sp = 0;
+                stk.put(L.T.sp++, make_uint2(0u, 0u));
+                L.state = M_LTRAV;
+                return;
+            }
+            next = shade_post(sc, L.r.d, m, scene_pdf_lp(sc, m.N, rtv::neg(L.r.d), m.r2, m.dir, 0.f), P, L.nv, L.r) &&
+                   L.power > 0;
+        }
+    } else {   // M_LREADY
+        const float4 q0 = mid[0], q1 = mid[ln], q2 = mid[2 * ln], q3 = mid[3 * ln], q4 = mid[4 * ln];
+        ShadeMid m;
+        m.pos = V3{q0.x, q0.y, q0.z};
+        m.r2 = q0.w;
+        m.N = V3{q1.x, q1.y, q1.z};
+        m.metallic = q1.w;
+        m.dir = V3{q2.x, q2.y, q2.z};
+        m.mesh = __float_as_int(q2.w);
+        m.tc = V2{q3.w, q4.x};
+        const V3 rd{q3.x, q3.y, q3.z};
+        P.set_e(L.nv - 1, P.get_e(L.nv - 1));
+        const float lp = L.T.acc / (float)sc.n_lights;
+        next = shade_post(sc, rd, m, scene_pdf_lp(sc, m.N, rtv::neg(rd), m.r2, m.dir, lp), P, L.nv, L.r) && L.power > 0;
+    }
+    if (next) L.power -= 1;
+    P.flush_e();
+    if (next) {
+        mega_begin<COUNT>(L, root, cnt);
+        return;
+    }
+    L.sum = rtv::add(L.sum, fold_path(P, L.nv));
+    if (++L.s == (FAST ? L.send : spp)) {
+        const long long o = FAST ? L.dst : L.pix;
+        out[3 * o + 0] = L.sum.x;
+        out[3 * o + 1] = L.sum.y;
+        out[3 * o + 2] = L.sum.z;
+        if (COUNT && !FAST && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
+        L.pix = -1;
+        L.state = M_IDLE;
+        return;
+    }
+    mega_sample<COUNT, FAST>(L, sc, g, root, cnt);
+}
+
 #if RT_TEAM && defined(__HIPCC__) && !RT_WIDE
 // The rest of lane `owner`'s ray by the whole wave (trav_team); false if its frames are not
 // all in LDS.  Then the owner is READY, as after its last trav_step.
@@ -206,10 +326,21 @@ __device__ __forceinline__ bool mega_team(MegaLane &L, int owner, const DevScene
 
 // One iteration of a wave's main loop for one lane, given the wave's decision: shade the
 // READY lanes this iteration (shade_now), or step the traversing lanes.
-template <bool COUNT, class Stack, class Nodes, bool FAST = false>
+template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT = false>
 __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
                                              const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt) {
+    if (LSPLIT) {
+        if (shade_now) {
+            if (L.state == M_READY || L.state == M_LREADY)
+                mega_shade_split<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt);
+            return;
+        }
+        if (L.state == M_LTRAV) {
+            if (light_step<COUNT>(sc, L.r, L.T, stk, cnt, st.mid + 2 * st.lanes + mega_slot())) L.state = M_LREADY;
+            return;
+        }
+    }
     if (shade_now) {
         if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, cnt);
     } else if (L.state == M_TRAV) {

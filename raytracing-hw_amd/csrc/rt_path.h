@@ -669,6 +669,7 @@ struct LaneRec {
         if (pending) A[v(ek)] = make_float4(e.x, e.y, e.z, 0.f);
         pending = false;
     }
+    __device__ __forceinline__ V3 get_e(int k) const { const float4 a = A[v(k)]; return V3{a.x, a.y, a.z}; }
 };
 // fold_path over LaneRec: the backward recurrence, records read four vertices at a time.
 __device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv) {
@@ -698,12 +699,23 @@ __device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv) {
     return c;
 }
 
-// One hit of Scene::intersect (scene.cpp:85-154): records vertex nv (its emission and, if
-// the path continues, its BRDF factors), advances nv and replaces r by the bounce ray.
-// Returns false where the recursion returns at this vertex (sample below the surface,
-// pdf <= 0 or NaN).
+// One hit of Scene::intersect (scene.cpp:85-154) in two halves around the light pdf, so the
+// light-BVH walk can run as its own traversal (rt_mega.h light_step):
+//   shade_pre  — emission (vertex nv), shading normal, metallic-roughness, the sampled
+//                direction, nv++ and the below-surface test; false where the recursion returns;
+//   shade_post — pdf from its parts, BRDF factors of vertex nv-1, the bounce ray; false where
+//                pdf <= 0 or NaN.
+// ShadeMid is what crosses the split (a lane-slot record in the lane-resident kernel).
+struct ShadeMid {
+    V3 pos, N, dir;
+    V2 tc;
+    float r2, metallic;
+    int mesh;
+};
+
 template <bool COUNT, class Rec>
-__device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
+__device__ __forceinline__ bool shade_pre(const DevScene &sc, const Ray &r, const Hit &hit, Rng &rng, Counters &cnt,
+                                          Rec &P, int &nv, ShadeMid &m) {
     RT_PROF_BEGIN
     if (COUNT) cnt.hits++;
     int id = hit.prim;
@@ -770,13 +782,36 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
         if (rtv::dot(dir, ngeo) <= 0.f) return false;
         N = ngeo;
     }
-    const float pdf = scene_pdf<COUNT>(sc, pos, N, eye, r2, dir, cnt);
-    RT_PROF_SEG(4);
+    m.pos = pos;
+    m.N = N;
+    m.dir = dir;
+    m.tc = tc;
+    m.r2 = r2;
+    m.metallic = metallic;
+    m.mesh = mesh;
+    return true;
+}
+
+// SceneDistribution::pdf (random.cpp:210-218) from a light pdf computed elsewhere.
+__device__ __forceinline__ float scene_pdf_lp(const DevScene &sc, V3 N, V3 eye, float r2, V3 dir, float lp) {
+    if (!sc.n_lights) return (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
+    return (cosine_pdf(N, dir) + lp + vndf_pdf(N, eye, r2, dir)) / 3;
+}
+
+template <class Rec>
+__device__ __forceinline__ bool shade_post(const DevScene &sc, const V3 rd, const ShadeMid &m, float pdf, Rec &P, int nv,
+                                           Ray &r_out) {
+    RT_PROF_BEGIN
     if (pdf <= 0.f || isnan(pdf)) return false;
+    const V3 pos = m.pos, N = m.N, dir = m.dir, eye = rtv::neg(rd);
+    const V2 tc = m.tc;
+    const float r2 = m.r2, metallic = m.metallic;
+    const float *mf = sc.mesh_f + 12 * m.mesh;
+    const int *mt = sc.mesh_tex + 4 * m.mesh;
     // BRDF of this vertex (scene.cpp:134-154): used only if the child ray hits
     const float coeff = 1 / pdf;
-    const V3 half = rtv::normal(rtv::sub(dir, r.d));
-    const float vis = smith(r2, N, eye, dir) * (1.f / (4 * fabsf(rtv::dot(N, r.d)) * fabsf(rtv::dot(N, dir))));
+    const V3 half = rtv::normal(rtv::sub(dir, rd));
+    const float vis = smith(r2, N, eye, dir) * (1.f / (4 * fabsf(rtv::dot(N, rd)) * fabsf(rtv::dot(N, dir))));
     const float spec = ggx(r2, N, half) * vis;
     const float VdotH = fabsf(rtv::dot(eye, half));
     V3 base{mf[0], mf[1], mf[2]};
@@ -789,9 +824,24 @@ __device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, 
     const V3 dielectric = rtv::add(rtv::mul(diffuse, 1 - dsc), rtv::mul(rtv::mul(V3{1.f, 1.f, 1.f}, spec), dsc));
     P.set_brdf(nv - 1, rtv::add(rtv::mul(dielectric, 1 - metallic), rtv::mul(metal, metallic)), coeff,
                rtv::dot(dir, N), mf[8]);
-    r = make_ray(rtv::add(pos, rtv::mul(dir, kStep)), dir);
+    r_out = make_ray(rtv::add(pos, rtv::mul(dir, kStep)), dir);
     RT_PROF_SEG(5);
     return true;
+}
+
+
+// The whole vertex in one piece (light pdf walked inline): records vertex nv (its emission
+// and, if the path continues, its BRDF factors), advances nv and replaces r by the bounce
+// ray.  Returns false where the recursion returns at this vertex (sample below the surface,
+// pdf <= 0 or NaN).
+template <bool COUNT, class Rec>
+__device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
+    ShadeMid m;
+    if (!shade_pre<COUNT>(sc, r, hit, rng, cnt, P, nv, m)) return false;
+    RT_PROF_BEGIN
+    const float pdf = scene_pdf<COUNT>(sc, m.pos, m.N, rtv::neg(r.d), m.r2, m.dir, cnt);
+    RT_PROF_SEG(4);
+    return shade_post(sc, r.d, m, pdf, P, nv, r);
 }
 
 // Backward fold over the recorded vertices (a primary miss gives bg colour 0).

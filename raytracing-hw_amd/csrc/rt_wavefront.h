@@ -25,6 +25,7 @@ struct WfState {
     float4 *rec_ab;   // AosRec: 2 per slot and vertex
     float *rec_c;     //         1 per slot and vertex
     long long lanes;  // lane-resident kernel: lane slots (LaneRec stride; rt_path.h)
+    float4 *mid;      // light-split kernel: shading state across the light walk, 5 per lane slot (rt_mega.h)
 };
 // meta: samples done (bits 0-19), depth budget left (20-23), vertices recorded (24-27),
 // normal cache valid (28)
@@ -324,6 +325,7 @@ struct TravState {
 // Where trav_step reads child pairs from: the node array in HBM ...
 struct GlobalNodes {
     static constexpr bool kPtr = true;   // pairs are plain memory (trav_step's shared load registers)
+    static constexpr bool kLdsTop = false;
     const float4 *node;
     __device__ __forceinline__ const float4 *pair(uint32_t left) const { return node + 2 * (size_t)left; }
     __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
@@ -423,9 +425,18 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
     RT_CHECK(!at_leaf || T.kend <= (uint32_t)sc.n_tris, 12, T.kend, T.k = T.kend = 1);
     float4 q[4 + 3 * (N - 1)];
     {
-        const float4 *p0 = at_node ? nodes.pair(T.a) : sc.tri + 3 * (size_t)(at_leaf ? k : 0u);
+        bool from_lds = false;
+        if constexpr (Nodes::kLdsTop) from_lds = at_node && Nodes::in_lds(T.a);
+        if (from_lds) {
+            if constexpr (Nodes::kLdsTop) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = p0[i];
+                for (int i = 0; i < 4; ++i) q[i] = Nodes::lds(T.a, i);
+            }
+        } else {
+            const float4 *p0 = at_node ? nodes.pair(T.a) : sc.tri + 3 * (size_t)(at_leaf ? k : 0u);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = p0[i];
+        }
 #pragma unroll
         for (int j = 1; j < N; ++j) {
             const uint32_t kj = at_leaf ? (k + j < klast ? k + j : klast) : 0u;
@@ -499,7 +510,7 @@ template <bool COUNT, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, const Nodes &nodes,
                                           Counters &cnt) {
     const bool at_node = T.phase == TP_NODE, at_leaf = T.phase == TP_LEAF;
-    if constexpr (RT_LEAF_N > 1 && Nodes::kPtr) return trav_step_n<COUNT>(sc, r, T, stk, nodes, cnt, at_node, at_leaf);
+    if constexpr (RT_LEAF_N > 1 && (Nodes::kPtr || Nodes::kLdsTop)) return trav_step_n<COUNT>(sc, r, T, stk, nodes, cnt, at_node, at_leaf);
     NodeRec L, R;
     V3 v0, U, V;
 #if RT_HOIST_LOADS
@@ -629,11 +640,18 @@ struct LdsStack {
 // ... or, for the top of the tree, LDS.  The device node array is breadth-first
 // (rt_device.hip bfs_nodes), so its first kLdsNodes nodes are the top levels, which nearly
 // every ray visits; each block keeps a copy and reads those pairs with ds_read.
-constexpr int kLdsNodes = 128;   // 4 KB: the top 7 levels of a full tree
+#ifndef RT_LDS_NODES
+#define RT_LDS_NODES 128
+#endif
+constexpr int kLdsNodes = RT_LDS_NODES;   // 128: 4 KB, the top 7 levels of a full tree
 __shared__ float4 wf_lds_nodes[2 * kLdsNodes];
 struct LdsNodes {
     static constexpr bool kPtr = false;
+    static constexpr bool kLdsTop = true;   // trav_step_n: pairs below kLdsNodes from LDS, the rest from `pair`
     const float4 *node;
+    __device__ __forceinline__ const float4 *pair(uint32_t left) const { return node + 2 * (size_t)left; }
+    __device__ __forceinline__ static bool in_lds(uint32_t left) { return left + 1 < (uint32_t)kLdsNodes; }
+    __device__ __forceinline__ static float4 lds(uint32_t left, int i) { return wf_lds_nodes[2 * left + i]; }
     __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
         if (left + 1 < (uint32_t)kLdsNodes) {
             const float4 p0 = wf_lds_nodes[2 * left], q0 = wf_lds_nodes[2 * left + 1];

@@ -224,8 +224,10 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
 
 // Emulates rt_mega_kernel (kernel 4): `waves` waves of 64 lanes, round-robin one main-loop
 // iteration at a time, sharing the pixel queue, with the kernel's shade_min decision.
-extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
-                              int shade_min, float *out, uint64_t *cnt_out) {
+// LSPLIT: the light-split kernel (light-pdf walk as lane states M_LTRAV / M_LREADY).
+template <bool LSPLIT>
+static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves, int shade_min,
+                       float *out, uint64_t *cnt_out) {
     rtd::DevScene sc = make(v);
     sc.n_tris = (int)v->n_tris;
     sc.n_nodes = (int)v->n_nodes;
@@ -244,6 +246,8 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
     st.rec_ab = ab.data();
     st.rec_c = cv.data();
     st.lanes = (long long)waves * 64;
+    std::vector<float4> mid((size_t)5 * st.lanes);
+    st.mid = mid.data();
     const rtd::NodeRec root = rtd::load_node(rtd::mega_nodes(sc), 0);
     const rtd::GlobalNodes nodes{sc.node};
     std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
@@ -277,8 +281,8 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
             int nr = 0, nt = 0;
             for (int l = 0; l < 64; ++l) {
                 any |= W[l].pix >= 0;
-                nr += W[l].state == rtd::M_READY;
-                nt += W[l].state == rtd::M_TRAV;
+                nr += W[l].state == rtd::M_READY || W[l].state == rtd::M_LREADY;
+                nt += W[l].state == rtd::M_TRAV || W[l].state == rtd::M_LTRAV;
             }
             if (!any) { done[w] = 1; --live; continue; }
             const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
@@ -289,13 +293,22 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
 #endif
                 rtd::g_mega_slot = (long long)w * 64 + l;
-                rtd::mega_iterate<true>(W[l], shade_now, sc, g, st, spp, out, nullptr, root, S, nodes, cnt);
+                rtd::mega_iterate<true, decltype(S), decltype(nodes), false, LSPLIT>(W[l], shade_now, sc, g, st, spp, out,
+                                                                                   nullptr, root, S, nodes, cnt);
             }
         }
     }
     uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
     std::memcpy(cnt_out, c, sizeof c);
     return 0;
+}
+extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
+                              int shade_min, float *out, uint64_t *cnt_out) {
+    return render_mega<false>(v, spp, rank, world, row_block, waves, shade_min, out, cnt_out);
+}
+extern "C" int kh_render_mega_lsplit(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
+                                     int shade_min, float *out, uint64_t *cnt_out) {
+    return render_mega<true>(v, spp, rank, world, row_block, waves, shade_min, out, cnt_out);
 }
 
 // box_pair_hit (rt_wavefront.h) against box_hit_pt on each box of the pair, over `n`

@@ -172,3 +172,19 @@ def test_fast_reciprocal_is_exact(gpu):
     """The traversal's 1/det (rt_wavefront.h rcp_ieee: v_rcp_f32 + one fma correction) equals
     the IEEE division for every float with a normal reciprocal (2^32 values on the device)."""
     assert gpu.device_selfcheck(0) == 0
+
+
+@pytest.mark.parametrize("split_min,name,w,h,s", [(1, "cornell", 64, 64, 8), (1, "sponza_mini", 64, 36, 4),
+                                                  (1, "cornell_blob", 48, 48, 4), (1, "practice6_1", 256, 256, 4),
+                                                  (64, "practice6_1", 256, 256, 4)])
+def test_light_split_kernel(gpu, monkeypatch, split_min, name, w, h, s):
+    """Light-split kernel (rt_mega.h light_step; off by default): forced on
+    (RT_LIGHT_SPLIT_MIN=1), and by threshold for practice6_1's 1,152 lights; bit-exact sums and
+    counters."""
+    monkeypatch.setenv("RT_LIGHT_SPLIT_MIN", str(split_min))
+    scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))   # knobs are read at upload
+    out, st = _sums(scene, s, count=True)
+    g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
+    assert np.array_equal(rtref.bits(out), rtref.bits(g["sums"].reshape(-1, 3)))
+    assert [st["rays"], st["aabb_tests"], st["tri_tests"], st["light_queries"], st["light_aabb_tests"],
+            st["light_tri_tests"]] == [int(x) for x in g["counters"]]

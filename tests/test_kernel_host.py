@@ -38,6 +38,8 @@ def _build_kh(tmp_path_factory, *defines):
     lib.kh_render_wf.restype = I
     lib.kh_render_mega.argtypes = [V, I, I, I, I, I, I, V, V]
     lib.kh_render_mega.restype = I
+    lib.kh_render_mega_lsplit.argtypes = [V, I, I, I, I, I, I, V, V]
+    lib.kh_render_mega_lsplit.restype = I
     lib.kh_box_pair_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
     lib.kh_box_pair_check.restype = ctypes.c_int64
     lib.kh_sqrt_gt_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
@@ -164,6 +166,22 @@ def test_lane_resident_emulation(rt, kh, name, w, h, s, waves, shade_min):
     out = np.zeros((h * w, 3), np.float32)
     cnt = np.zeros(7, np.uint64)
     assert kh.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data, cnt.ctypes.data) == 0
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert list(cnt[:6]) == list(cnt_want)
+
+
+@pytest.mark.parametrize("name,w,h,s,waves,shade_min", [("practice6_1", 256, 256, 4, 6, 48), ("sponza_mini", 64, 36, 4, 3, 1),
+                                                        ("cornell", 33, 17, 3, 1, 64)])
+def test_lane_resident_light_split_emulation(rt, kh, name, w, h, s, waves, shade_min):
+    """Light-split kernel (rt_mega.h light_step / mega_shade_split): the
+    light pdf's light-BVH walk as a lane state between shade_pre and shade_post; bit-exact
+    sums and reference counters (practice6_1: 1,152 emissive triangles)."""
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    out = np.zeros((h * w, 3), np.float32)
+    cnt = np.zeros(7, np.uint64)
+    assert kh.kh_render_mega_lsplit(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data,
+                                    cnt.ctypes.data) == 0
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert list(cnt[:6]) == list(cnt_want)
 
