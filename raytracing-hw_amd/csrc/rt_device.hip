@@ -956,7 +956,9 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const bool lsplit = !fast && d->ds.n_lights >= d->light_split_min && d->light_split_min > 0;
             auto pick = [&](int wpe) {
                 if (fast) return count ? rt_mega_kernel<true, 5, true> : rt_mega_kernel<false, 5, true>;
+#if !RT_WIDE
                 if (lsplit) return count ? rt_mega_kernel<true, 5, false, true> : rt_mega_kernel<false, 5, false, true>;
+#endif
                 switch (wpe) {
                     case 5: return count ? rt_mega_kernel<true, 5> : rt_mega_kernel<false, 5>;
                     case 6: return count ? rt_mega_kernel<true, 6> : rt_mega_kernel<false, 6>;

@@ -330,7 +330,7 @@ template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT =
 __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
                                              const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt) {
-    if (LSPLIT) {
+    if constexpr (LSPLIT) {   // (not with RT_WIDE: the light walk uses TravState and the pair stack)
         if (shade_now) {
             if (L.state == M_READY || L.state == M_LREADY)
                 mega_shade_split<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt);

@@ -308,7 +308,11 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
 }
 extern "C" int kh_render_mega_lsplit(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
                                      int shade_min, float *out, uint64_t *cnt_out) {
+#if RT_WIDE
+    return -1;   // the light-split path is built without RT_WIDE only
+#else
     return render_mega<true>(v, spp, rank, world, row_block, waves, shade_min, out, cnt_out);
+#endif
 }
 
 // box_pair_hit (rt_wavefront.h) against box_hit_pt on each box of the pair, over `n`
