@@ -213,11 +213,12 @@ def main():
             fast_ms.append(step(fast=True)["render_ms"])
         torch.cuda.synchronize()
         barrier()
-        tf = torch.tensor([time.perf_counter() - tf, float(fc["rays"])], dtype=torch.float64, device="cuda")
+        t_fast = torch.tensor([time.perf_counter() - tf], dtype=torch.float64, device="cuda")
+        r_fast = torch.tensor([float(fc["rays"])], dtype=torch.float64, device="cuda")
         if world > 1:
-            dist.all_reduce(tf[0:1], op=dist.ReduceOp.MAX)
-            dist.all_reduce(tf[1:2], op=dist.ReduceOp.SUM)
-        fe, frays = float(tf[0].item()), float(tf[1].item())
+            dist.all_reduce(t_fast, op=dist.ReduceOp.MAX)
+            dist.all_reduce(r_fast, op=dist.ReduceOp.SUM)
+        fe, frays = float(t_fast.item()), float(r_fast.item())
         fast_line = {"value": round(frays * args.fast_steps / fe / 1e6, 3), "unit": "Mrays/s",
                      "ms_per_step": round(fe / args.fast_steps * 1e3, 3), "steps": args.fast_steps,
                      "chunk": args.fast_chunk, "rays_per_frame": int(frays),
