@@ -128,6 +128,35 @@ __device__ __forceinline__ Rng lane_rng(const MegaLane &L) { return L.rng; }
 __device__ __forceinline__ void lane_rng_set(MegaLane &L, const Rng &r) { L.rng = r; }
 #endif
 
+// RT_MEGA_LDS_CTR: the lane's sample counter, depth budget and recorded-vertex count live in
+// LDS (3 KB per block); shading loads them once and stores them back (A/B knob).
+#ifndef RT_MEGA_LDS_CTR
+#define RT_MEGA_LDS_CTR 0
+#endif
+struct LaneCtr {
+    int s, power, nv;
+};
+#if RT_MEGA_LDS_CTR && defined(__HIPCC__)
+__shared__ int mega_lds_ctr[3 * 256];
+__device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &) {
+    const int t = threadIdx.x;
+    return LaneCtr{mega_lds_ctr[t], mega_lds_ctr[256 + t], mega_lds_ctr[512 + t]};
+}
+__device__ __forceinline__ void lane_ctr_set(MegaLane &, const LaneCtr &c) {
+    const int t = threadIdx.x;
+    mega_lds_ctr[t] = c.s;
+    mega_lds_ctr[256 + t] = c.power;
+    mega_lds_ctr[512 + t] = c.nv;
+}
+#else
+__device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &L) { return LaneCtr{L.s, L.power, L.nv}; }
+__device__ __forceinline__ void lane_ctr_set(MegaLane &L, const LaneCtr &c) {
+    L.s = c.s;
+    L.power = c.power;
+    L.nv = c.nv;
+}
+#endif
+
 // Closest-hit query start for L.r: BVH::intersect's counters and root box (bvh.cpp:239-243).
 template <bool COUNT>
 __device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Counters &cnt) {
@@ -146,10 +175,12 @@ __device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Cou
 template <bool COUNT, bool FAST = false>
 __device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
                                             Counters &cnt) {
-    Rng rng = FAST ? Rng{fast_sample_seed(L.gpix, (uint32_t)L.s), 0u, 0.f} : lane_rng(L);
-    L.r = start_sample(sc, g, L.pix, rng, L.power);
+    LaneCtr c = lane_ctr(L);
+    Rng rng = FAST ? Rng{fast_sample_seed(L.gpix, (uint32_t)c.s), 0u, 0.f} : lane_rng(L);
+    L.r = start_sample(sc, g, L.pix, rng, c.power);
     lane_rng_set(L, rng);
-    L.nv = 0;
+    c.nv = 0;
+    lane_ctr_set(L, c);
     mega_begin<COUNT>(L, root, cnt);
 }
 
@@ -158,7 +189,7 @@ template <bool COUNT>
 __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, const ShardGeom &g, long long p,
                                             const NodeRec &root, Counters &cnt) {
     L.pix = p;
-    L.s = 0;
+    lane_ctr_set(L, LaneCtr{0, 0, 0});
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
     L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
     const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
@@ -176,8 +207,9 @@ __device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc
     const long long c = q / g.n_pixels, p = q - c * g.n_pixels;
     L.pix = p;
     L.dst = q;
-    L.s = (int)c * cs;
-    L.send = L.s + cs < spp ? L.s + cs : spp;
+    const int s0 = (int)c * cs;
+    lane_ctr_set(L, LaneCtr{s0, 0, 0});
+    L.send = s0 + cs < spp ? s0 + cs : spp;
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
     const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
     L.gpix = (uint32_t)(py * sc.width + px);
@@ -195,24 +227,26 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
     AosRec P{st.rec_ab, st.rec_c, L.pix, st.D, V3{0.f, 0.f, 0.f}, 0, false};
 #endif
     const Hit h = L.T.best;
+    LaneCtr c = lane_ctr(L);
     bool next = false;
     if (h.prim >= 0 && h.t < sc.max_distance) {
         Rng rng = lane_rng(L);
-        const bool cont = shade_hit<COUNT>(sc, L.r, h, rng, cnt, P, L.nv);
+        const bool cont = shade_hit<COUNT>(sc, L.r, h, rng, cnt, P, c.nv);
         lane_rng_set(L, rng);
-        if (cont && L.power > 0) {
-            L.power -= 1;
+        if (cont && c.power > 0) {
+            c.power -= 1;
             next = true;
         }
     }
     P.flush_e();
     if (next) {
+        lane_ctr_set(L, c);
         mega_begin<COUNT>(L, root, cnt);
         return;
     }
-    const V3 sm = rtv::add(lane_sum(L), fold_path(P, L.nv));
+    const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv));
     lane_sum_set(L, sm);
-    if (++L.s == (FAST ? L.send : spp)) {
+    if (++c.s == (FAST ? L.send : spp)) {
         const long long o = FAST ? L.dst : L.pix;
         out[3 * o + 0] = sm.x;
         out[3 * o + 1] = sm.y;
@@ -222,6 +256,7 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
         L.state = M_IDLE;
         return;
     }
+    lane_ctr_set(L, c);
     mega_sample<COUNT, FAST>(L, sc, g, root, cnt);
 }
 
@@ -286,6 +321,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
     LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, slot, st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     float4 *mid = st.mid + slot;
     const long long ln = st.lanes;
+    LaneCtr c = lane_ctr(L);
     bool next = false;
     if (L.state == M_READY) {
         const Hit h = L.T.best;
@@ -293,7 +329,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
         bool pre = false;
         if (h.prim >= 0 && h.t < sc.max_distance) {
             Rng rng = lane_rng(L);
-            pre = shade_pre<COUNT>(sc, L.r, h, rng, cnt, P, L.nv, m);
+            pre = shade_pre<COUNT>(sc, L.r, h, rng, cnt, P, c.nv, m);
             lane_rng_set(L, rng);
         }
         if (pre) {
@@ -310,10 +346,11 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
                 L.T.sp = 0;
                 stk.put(L.T.sp++, make_uint2(0u, 0u));
                 L.state = M_LTRAV;
+                lane_ctr_set(L, c);
                 return;
             }
-            next = shade_post(sc, L.r.d, m, scene_pdf_lp(sc, m.N, rtv::neg(L.r.d), m.r2, m.dir, 0.f), P, L.nv, L.r) &&
-                   L.power > 0;
+            next = shade_post(sc, L.r.d, m, scene_pdf_lp(sc, m.N, rtv::neg(L.r.d), m.r2, m.dir, 0.f), P, c.nv, L.r) &&
+                   c.power > 0;
         }
     } else {   // M_LREADY
         const float4 q0 = mid[0], q1 = mid[ln], q2 = mid[2 * ln], q3 = mid[3 * ln], q4 = mid[4 * ln];
@@ -326,19 +363,20 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
         m.mesh = __float_as_int(q2.w);
         m.tc = V2{q3.w, q4.x};
         const V3 rd{q3.x, q3.y, q3.z};
-        P.set_e(L.nv - 1, P.get_e(L.nv - 1));
+        P.set_e(c.nv - 1, P.get_e(c.nv - 1));
         const float lp = L.T.acc / (float)sc.n_lights;
-        next = shade_post(sc, rd, m, scene_pdf_lp(sc, m.N, rtv::neg(rd), m.r2, m.dir, lp), P, L.nv, L.r) && L.power > 0;
+        next = shade_post(sc, rd, m, scene_pdf_lp(sc, m.N, rtv::neg(rd), m.r2, m.dir, lp), P, c.nv, L.r) && c.power > 0;
     }
-    if (next) L.power -= 1;
+    if (next) c.power -= 1;
     P.flush_e();
     if (next) {
+        lane_ctr_set(L, c);
         mega_begin<COUNT>(L, root, cnt);
         return;
     }
-    const V3 sm = rtv::add(lane_sum(L), fold_path(P, L.nv));
+    const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv));
     lane_sum_set(L, sm);
-    if (++L.s == (FAST ? L.send : spp)) {
+    if (++c.s == (FAST ? L.send : spp)) {
         const long long o = FAST ? L.dst : L.pix;
         out[3 * o + 0] = sm.x;
         out[3 * o + 1] = sm.y;
@@ -348,6 +386,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
         L.state = M_IDLE;
         return;
     }
+    lane_ctr_set(L, c);
     mega_sample<COUNT, FAST>(L, sc, g, root, cnt);
 }
 
