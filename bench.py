@@ -126,7 +126,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fast-steps", type=int, default=2,
                     help="timed frames of fast mode (RT_FLAG_FAST, reported beside the headline; 0 = skip)")
-    ap.add_argument("--fast-chunk", type=int, default=16, help="fast mode: samples per work unit")
+    ap.add_argument("--fast-chunk", type=int, default=2, help="fast mode: samples per work unit")
     ap.add_argument("--traffic-from", default="auto",
                     help="PMC summaries for roofline.traffic: a path prefix P (P_fetch*.csv / P_write*.csv from "
                          "tools/profile.sh of this same command), 'auto' (the committed profiles/ pair when the "

@@ -89,7 +89,7 @@ typedef struct {
     int32_t kernel;       /* 0 = lane-resident (default), 1 = one lane per pixel, 2 = persistent per-pixel,
                              3 = wave megakernel, 4 = wavefront (extend/shade launches) */
     int32_t flags;        /* RT_FLAG_* */
-    int32_t fast_chunk;   /* RT_FLAG_FAST: samples per work unit (0 = 16)                 */
+    int32_t fast_chunk;   /* RT_FLAG_FAST: samples per work unit (0 = 2)                  */
 } rt_params;
 
 /* rt_params.flags */

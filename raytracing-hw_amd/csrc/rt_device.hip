@@ -947,7 +947,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "ray_depth must be in [1, 15]");
             // fast mode (RT_FLAG_FAST): work units of `cs` samples, Philox seed per sample
             const bool fast = (p->flags & RT_FLAG_FAST) != 0;
-            const int cs = fast ? std::min(spp, p->fast_chunk > 0 ? p->fast_chunk : 16) : 0;
+            const int cs = fast ? std::min(spp, p->fast_chunk > 0 ? p->fast_chunk : 2) : 0;
             const int chunks = fast ? (spp + cs - 1) / cs : 1;
             const long long n_items = g.n_pixels * chunks;
             if (fast && n_items > (long long)UINT32_MAX - 65536)
