@@ -261,7 +261,7 @@ def main():
             prefix = args.traffic_from
             default_cfg = (args.scene, W, H, S, args.kernel) == ("sponza", 1920, 1080, 256, 0)
             if prefix == "auto":
-                prefix = os.path.join(ROOT, "profiles", "r01b_final") if default_cfg else None
+                prefix = os.path.join(ROOT, "profiles", "r01c_final") if default_cfg else None
             if prefix:
                 fc, wc = prefix + "_fetch_1080p256.csv", prefix + "_write_1080p256.csv"
                 if os.path.exists(fc) and os.path.exists(wc):
