@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                     const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
                     if (p < n_items) {
                         if (FAST) rtd::mega_assign_fast<COUNT>(L, sc, g, p, cs, spp, root, cnt);
-                        else rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : p, root, cnt);
+                        else rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
                     }
                 }
                 if ((long long)base + cm >= n_items) exhausted = true;
@@ -912,6 +912,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
     if ((p->flags & RT_FLAG_FAST) && p->kernel != 0)
         return rt_fail(RT_ERR_ARG, "rt_render: fast mode (RT_FLAG_FAST) runs on kernel 0 only");
     if (p->fast_chunk < 0) return rt_fail(RT_ERR_ARG, "rt_render: fast_chunk must be >= 0");
+    if ((int64_t)s->width * s->height > INT32_MAX)
+        return rt_fail(RT_ERR_LIMIT, "rt_render: frames above 2^31 pixels are not supported");
     const int64_t rows = rt_shard_rows_impl(s->height, rank, world, rb, nullptr);
     if (rows < 0) return RT_ERR_ARG;
     ShardGeom g{s->width, rank, world, rb, (long long)rows * s->width};

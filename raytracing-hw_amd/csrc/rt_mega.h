@@ -67,7 +67,7 @@ __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return
 enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4 };
 
 struct MegaLane {
-    long long pix;   // shard pixel (slot), -1 = none
+    int pix;         // shard pixel (slot), -1 = none (the host keeps shards below 2^31 pixels)
     int s, power, nv, state;
     // fast mode only (RT_FLAG_FAST): work unit = samples [s, send) of the pixel; its partial
     // sum goes to dst; gpix = j*W+i keys the per-sample Philox seed.  Unused fields of the
@@ -157,6 +157,27 @@ __device__ __forceinline__ void lane_ctr_set(MegaLane &L, const LaneCtr &c) {
 }
 #endif
 
+// RT_MEGA_UV_RECOMPUTE: shading recomputes the winner's barycentrics (the traversal's own
+// tri_hit_bl on the same ray and triangle: the same bits), so TravState's best.u / best.v
+// are never read and the traversal stops carrying them (A/B knob).
+#ifndef RT_MEGA_UV_RECOMPUTE
+#define RT_MEGA_UV_RECOMPUTE 0
+#endif
+__device__ __forceinline__ Hit mega_best(const MegaLane &L, const DevScene &sc) {
+    Hit h = L.T.best;
+#if RT_MEGA_UV_RECOMPUTE
+    if (h.prim >= 0) {
+        const float4 *q = sc.tri + 3 * (size_t)h.prim;
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+        TriHit th;
+        tri_hit_bl(V3{q0.x, q0.y, q0.z}, V3{q0.w, q1.x, q1.y}, V3{q1.z, q1.w, q2.x}, L.r, th);
+        h.u = th.u;
+        h.v = th.v;
+    }
+#endif
+    return h;
+}
+
 // Closest-hit query start for L.r: BVH::intersect's counters and root box (bvh.cpp:239-243).
 template <bool COUNT>
 __device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Counters &cnt) {
@@ -177,7 +198,13 @@ __device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, con
                                             Counters &cnt) {
     LaneCtr c = lane_ctr(L);
     Rng rng = FAST ? Rng{fast_sample_seed(L.gpix, (uint32_t)c.s), 0u, 0.f} : lane_rng(L);
-    L.r = start_sample(sc, g, L.pix, rng, c.power);
+    {   // start_sample (rt_wavefront.h) with 32-bit pixel arithmetic
+        const int k = L.pix / g.width, px = L.pix - k * g.width, py = shard_row(g, k);
+        const float ox = rng_offset(rng);
+        const float oy = rng_offset(rng);
+        c.power = sc.ray_depth - 1;
+        L.r = camera_ray(sc, px, py, ox, oy);
+    }
     lane_rng_set(L, rng);
     c.nv = 0;
     lane_ctr_set(L, c);
@@ -186,13 +213,13 @@ __device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, con
 
 // A new pixel: seed its RNG (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1), first sample.
 template <bool COUNT>
-__device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, const ShardGeom &g, long long p,
+__device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, const ShardGeom &g, int p,
                                             const NodeRec &root, Counters &cnt) {
     L.pix = p;
     lane_ctr_set(L, LaneCtr{0, 0, 0});
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
     L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
-    const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
+    const int k = p / g.width, px = p - k * g.width, py = shard_row(g, k);
     const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
     lane_rng_set(L, Rng{seed == 0 ? 1u : seed, 0u, 0.f});
     mega_sample<COUNT>(L, sc, g, root, cnt);
@@ -204,14 +231,15 @@ __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, con
 template <bool COUNT>
 __device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc, const ShardGeom &g, long long q,
                                                  int cs, int spp, const NodeRec &root, Counters &cnt) {
-    const long long c = q / g.n_pixels, p = q - c * g.n_pixels;
+    const long long c = q / g.n_pixels;
+    const int p = (int)(q - c * g.n_pixels);
     L.pix = p;
     L.dst = q;
     const int s0 = (int)c * cs;
     lane_ctr_set(L, LaneCtr{s0, 0, 0});
     L.send = s0 + cs < spp ? s0 + cs : spp;
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
-    const int k = (int)(p / g.width), px = (int)(p % g.width), py = shard_row(g, k);
+    const int k = p / g.width, px = p - k * g.width, py = shard_row(g, k);
     L.gpix = (uint32_t)(py * sc.width + px);
     mega_sample<COUNT, true>(L, sc, g, root, cnt);
 }
@@ -226,7 +254,7 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
 #else
     AosRec P{st.rec_ab, st.rec_c, L.pix, st.D, V3{0.f, 0.f, 0.f}, 0, false};
 #endif
-    const Hit h = L.T.best;
+    const Hit h = mega_best(L, sc);
     LaneCtr c = lane_ctr(L);
     bool next = false;
     if (h.prim >= 0 && h.t < sc.max_distance) {
@@ -324,7 +352,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
     LaneCtr c = lane_ctr(L);
     bool next = false;
     if (L.state == M_READY) {
-        const Hit h = L.T.best;
+        const Hit h = mega_best(L, sc);
         ShadeMid m;
         bool pre = false;
         if (h.prim >= 0 && h.t < sc.max_distance) {
