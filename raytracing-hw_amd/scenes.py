@@ -590,7 +590,45 @@ def _sponza_primitive(mat: int, budget: int, lo, hi, rng) -> tuple:
     return acc.arrays()
 
 
-def make_sponza(directory: str, tri_scale: float = 1.0, tex_size: int = 1024, name: str = "sponza") -> str:
+DRAGON_FIXTURE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                              "dragon10k_tris.npy")
+
+
+def dragon_100k() -> np.ndarray:
+    """C5's dragon proxy (SURVEY.md §7, §8 C5): the 9,992 triangles of the reference's
+    practice5_dragon_10k.txt (tests/golden/dragon10k_tris.npy, tools/make_dragon_fixture.py),
+    1->4 midpoint subdivision, then the first 20,011 of those again: 100,001 triangles,
+    (n, 3, 3) float32, in the fixture's coordinates."""
+    def split(t):
+        a, b, c = t[:, 0], t[:, 1], t[:, 2]
+        ab, bc, ca = (a + b) * 0.5, (b + c) * 0.5, (c + a) * 0.5
+        return np.stack([np.stack([a, ab, ca], 1), np.stack([ab, b, bc], 1), np.stack([ca, bc, c], 1),
+                         np.stack([ab, bc, ca], 1)], 1).reshape(-1, 3, 3)
+    t = split(np.load(DRAGON_FIXTURE).astype(np.float64))
+    k = 20011
+    return np.concatenate([split(t[:k]), t[k:]]).astype(np.float32)
+
+
+def _dragon_in_sponza(b: "GltfBuilder") -> None:
+    """The dragon on the sponza proxy's floor, 5 m in front of its camera (scale 0.25,
+    flat normals, one untextured metallic material)."""
+    t = dragon_100k().astype(np.float64)
+    lo = t.reshape(-1, 3).min(0)
+    t = (t - np.array([0.0, lo[1], 0.0])) * 0.25 + np.array([5.0, 0.0, -0.6])
+    n = np.cross(t[:, 1] - t[:, 0], t[:, 2] - t[:, 0])
+    n /= np.maximum(np.linalg.norm(n, axis=1, keepdims=True), 1e-30)
+    pos = t.reshape(-1, 3)
+    nrm = np.repeat(n, 3, axis=0)
+    idx = np.arange(pos.shape[0])
+    mat = len(b.materials)
+    b.materials.append({"name": "Dragon", "pbrMetallicRoughness": {
+        "baseColorFactor": [0.72, 0.52, 0.3, 1], "metallicFactor": 0.6, "roughnessFactor": 0.35}})
+    mesh = b.mesh("Dragon", [b.primitive(pos, nrm, idx, mat)])
+    b.nodes.append({"mesh": mesh, "name": "Dragon"})
+
+
+def make_sponza(directory: str, tri_scale: float = 1.0, tex_size: int = 1024, name: str = "sponza",
+                dragon: bool = False) -> str:
     b = GltfBuilder()
     b.extensions_used.add(_EMISSIVE)
     b.nodes = [dict(n) for n in SPONZA_NODES]
@@ -613,6 +651,8 @@ def make_sponza(directory: str, tri_scale: float = 1.0, tex_size: int = 1024, na
         path = os.path.join(directory, fname)
         write_ppm(path, _procedural_texture(img, roles.get(img, "base"), tex_size))
     b.textures = [{"sampler": 0, "source": s} for s in SPONZA_TEXTURE_SOURCES]
+    if dragon:
+        _dragon_in_sponza(b)
     return b.write(directory, name)
 
 
@@ -622,6 +662,10 @@ SCENES = {
     "practice6_1": lambda d: make_practice6_1(d),
     "sponza_mini": lambda d: make_sponza(d, tri_scale=1.0 / 32, tex_size=16, name="sponza_mini"),
     "sponza": lambda d: make_sponza(d),
+    # BASELINE.json configs[4] (C5): dragon-100k proxy + sponza proxy
+    "sponza_dragon": lambda d: make_sponza(d, dragon=True, name="sponza_dragon"),
+    "sponza_dragon_mini": lambda d: make_sponza(d, tri_scale=1.0 / 32, tex_size=16, name="sponza_dragon_mini",
+                                                dragon=True),
 }
 
 

@@ -188,3 +188,23 @@ def test_light_split_kernel(gpu, monkeypatch, split_min, name, w, h, s):
     assert np.array_equal(rtref.bits(out), rtref.bits(g["sums"].reshape(-1, 3)))
     assert [st["rays"], st["aabb_tests"], st["tri_tests"], st["light_queries"], st["light_aabb_tests"],
             st["light_tri_tests"]] == [int(x) for x in g["counters"]]
+
+
+@pytest.mark.parametrize("name,W,H", [("sponza_dragon_mini", 96, 54), ("sponza_dragon", 3840, 2160)])
+def test_sponza_dragon_c5_pixels_vs_oracle(gpu, oracle, name, W, H):
+    """BASELINE.json configs[4] (C5: dragon-100k proxy + sponza proxy, 3840x2160): a seeded
+    sample of pixels, GPU vs the CPU oracle on the very same flattened scene (2 spp)."""
+    scenes = rtref.scenes_module()
+    import tempfile, os
+    path = scenes.ensure_scene(name, os.path.join(tempfile.gettempdir(), "rt_scenes"))
+    S = 2
+    scene = gpu.Scene.load(path, W, H, S)
+    out, st = scene.render_sums(S, count=True)
+    out = out.reshape(-1, 3)
+    assert st["rays"] >= W * H * S
+    arrays = scene.view()
+    rng = np.random.default_rng(11)
+    pix = rng.choice(W * H, 40, replace=False) if W * H > 10000 else np.arange(W * H)
+    for p in pix:
+        ref, _, _ = oracle.render(arrays, S, int(p), int(p) + 1, threads=1)
+        assert np.array_equal(rtref.bits(out[p]), rtref.bits(ref[0])), f"pixel {p}"
