@@ -615,7 +615,10 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
 // Device stack: the first K entries in LDS (entry k of thread t at [k * 256 + t], so a
 // wave's 64 lanes hit consecutive 8-byte words), deeper entries in scratch.  K = 8 holds
 // 96% of all pushes on the sponza frame (tools: RT_STACK_PROBE histogram).
-constexpr int kLdsStack = 8;
+#ifndef RT_LDS_STACK
+#define RT_LDS_STACK 8
+#endif
+constexpr int kLdsStack = RT_LDS_STACK;   // stack frames per lane in LDS (deeper ones spill to scratch)
 __shared__ uint2 wf_lds_stack[kLdsStack * 256];   // blocks of 256 threads
 struct LdsStack {
     uint2 *spill;   // this thread's private overflow array (scratch), kStack - kLdsStack entries
