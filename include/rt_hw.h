@@ -9,6 +9,8 @@
  *   rt_render / rt_render_device
  *                        <- Scene::render sample loop   src/core/scene.cpp:17-52
  *                           (per-pixel float RGB sums = sample_canvas, scene.cpp:20,42)
+ *   rt_render_multi      <- the same loop over every GPU of the node (one row-block shard
+ *                           per device, frame assembled on the host)
  *   rt_tonemap_u8        <- Scene::render frame finish  src/core/scene.cpp:54-64
  *   rt_tonemap_u8_device <- the same finish on the GPU   src/core/scene.cpp:54-64
  *   rt_write_ppm         <- Canvas::write_to            src/render/canvas.h:76-89
@@ -31,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum rt_status {
     RT_OK = 0,
@@ -86,11 +88,17 @@ typedef struct {
     int32_t rank, world;  /* pixel-row partition: rows whose (row / row_block) % world == rank */
     int32_t row_block;    /* rows per interleave block (default 8)                       */
     int32_t count;        /* 1 = accumulate ray / AABB / triangle test counters          */
-    int32_t kernel;       /* 0 = lane-resident (default), 1 = one lane per pixel, 2 = persistent per-pixel,
-                             3 = wave megakernel, 4 = wavefront (extend/shade launches) */
+    int32_t kernel;       /* RT_KERNEL_LANE (0, default) or RT_KERNEL_WAVEFRONT (4)      */
     int32_t flags;        /* RT_FLAG_* */
-    int32_t fast_chunk;   /* RT_FLAG_FAST: samples per work unit (0 = 2)                  */
+    int32_t fast_chunk;   /* RT_FLAG_FAST: samples per work unit (0 = 2; raised so a pixel
+                             has at most 128 units)                                      */
+    int32_t device;       /* HIP device to render on (rt_render uploads the scene there;
+                             rt_render_device needs rt_scene_upload(scene, device) first) */
 } rt_params;
+
+/* rt_params.kernel: two schedules of the same per-pixel arithmetic (same bits) */
+#define RT_KERNEL_LANE 0       /* lane-resident persistent kernel (rt_mega.h)            */
+#define RT_KERNEL_WAVEFRONT 4  /* wavefront: init / extend / shade launches (rt_wavefront.h) */
 
 /* rt_params.flags */
 #define RT_FLAG_KERNEL_TIMES 1  /* wavefront path (kernel 4): time every extend / shade launch (HIP events) */
@@ -98,9 +106,17 @@ typedef struct {
  * stream (Philox4x32-10 keyed by pixel j*W+i, counter = sample, seeds the sample's minstd
  * stream; normal cache empty per sample), so a pixel's samples are independent work units
  * of fast_chunk samples that any lane may run.  The pixel sum is the chunk partials added in
- * chunk order: deterministic for a given fast_chunk, statistically equivalent to the
+ * chunk order: deterministic for a given (spp, fast_chunk), statistically equivalent to the
  * reference, NOT bit-identical to it (the parity mode is the default). */
 #define RT_FLAG_FAST 2
+/* Light-split kernel (kernel 0, parity mode): the light pdf's light-BVH
+ * walk as its own traversal state between two shading passes.  Same bits; measured slower
+ * on every scene tried, so off by default. */
+#define RT_FLAG_LIGHT_SPLIT 4
+/* Parity mode renders pixels heaviest-first: a counting pre-pass of 2 samples per pixel
+ * (its own Philox streams), a radix sort and a spread over the waves, all inside the call
+ * and inside render_ms.  This flag renders in row-major order instead (same bits). */
+#define RT_FLAG_NATURAL_ORDER 8
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */
@@ -112,11 +128,15 @@ typedef struct {
     uint64_t light_aabb_tests;
     uint64_t light_tri_tests;
     uint64_t shading_hits;  /* scene hits that were shaded (texture / attribute fetches)  */
-    double render_ms;       /* device time of the render kernel(s), HIP events            */
+    double render_ms;       /* device time of the whole render (order pre-pass included), HIP events;
+                               rt_render_multi: the slowest device                           */
     /* RT_FLAG_KERNEL_TIMES (wavefront path): summed launch durations and launch counts   */
     double extend_ms, shade_ms;
     uint64_t extend_launches, shade_launches;
     uint64_t extend_rays;   /* rays traced by the extend launches (always filled)          */
+    double order_ms;        /* part of render_ms spent building the pixel order            */
+    double gather_ms;       /* rt_render_multi: host assembly of the frame (slowest device) */
+    uint64_t devices;       /* devices that rendered                                       */
 } rt_stats;
 
 /* --- scene ------------------------------------------------------------------------ */
@@ -129,7 +149,8 @@ int rt_scene_get_view(const rt_scene *scene, rt_scene_view *view);
 void rt_scene_free(rt_scene *scene);
 
 /* --- render ----------------------------------------------------------------------- */
-/* Copies the scene to `device` (once; later calls reuse it). */
+/* Copies the scene to `device` (once per device; later calls reuse it).  One render per
+ * (scene, device) may be in flight at a time; different devices render independently. */
 int rt_scene_upload(rt_scene *scene, int32_t device);
 /* Number of pixels a (rank, world, row_block) shard owns, and their row-major order:
  * rows_out (may be NULL) receives the owned row indices, ascending. */
@@ -140,6 +161,11 @@ int rt_render(rt_scene *scene, const rt_params *params, float *out_sum, rt_stats
  * `stream` (NULL = default stream); returns after the launch (asynchronous) unless
  * stats != NULL, in which case it waits and fills the counters and kernel time. */
 int rt_render_device(rt_scene *scene, const rt_params *params, float *d_out_sum, void *stream, rt_stats *stats);
+/* The whole frame on devices 0 .. n_devices-1 (n_devices <= 0: every visible device), one
+ * host thread per device, device d rendering the shard (rank d, world n_devices,
+ * params->row_block); params->rank / world / device are ignored.  out_sum: W*H*3 floats,
+ * host memory, row-major.  Bits do not depend on n_devices. */
+int rt_render_multi(rt_scene *scene, const rt_params *params, int32_t n_devices, float *out_sum, rt_stats *stats);
 
 /* Closest hit + light pdf for n explicit rays (BVH::intersect bvh.cpp:239-243 and
  * ManyLightsDistribution::pdf random.cpp:179-188; origin/dir as given to Ray::Ray, which

@@ -15,6 +15,9 @@
 //   rays    <gltf> W H n out.rtd               closest-hit known answers (bvh.cpp:239-243) + per-ray test counts
 //   dump    <gltf> W H out.rtd                 post-BVH scene arrays (bvh.cpp:166 reorders objects)
 //   samplers <gltf> W H n out.rtd              SceneDistribution::sample/pdf + RNG known answers
+//   pixels  <gltf> W H spp idx.i64 out.rtd [threads]
+//                                              per-pixel sums of the listed frame pixels (raw int64
+//                                              indices j*W+i) at full spp, + per-pixel test counts
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -195,6 +198,54 @@ static int mode_time(int argc, char **argv) {
     char extra[128];
     std::snprintf(extra, sizeof extra, ", \"pixels\": %lld, \"spp\": %d", (long long)W * rows, spp);
     print_counts("time", total_counters(), t1 - t0, omp_get_max_threads(), extra);
+    return 0;
+}
+
+// Listed pixels of a frame at full spp (any W x H x spp, e.g. BASELINE's C3-C5): the same
+// per-pixel loop as `sums` (render_pixel) on a subset, with per-pixel counters (the counting
+// wraps count per thread and a pixel runs on one thread, so the difference is the pixel's).
+static int mode_pixels(int argc, char **argv) {
+    if (argc < 8) throw std::runtime_error("pixels <gltf> W H spp idx.i64 out.rtd [threads]");
+    int W = atoi(argv[3]), H = atoi(argv[4]), spp = atoi(argv[5]);
+    int threads = argc > 8 ? atoi(argv[8]) : omp_get_max_threads();
+    std::FILE *f = std::fopen(argv[6], "rb");
+    if (!f) throw std::runtime_error(std::string("cannot open ") + argv[6]);
+    std::vector<int64_t> idx;
+    int64_t v;
+    while (std::fread(&v, sizeof v, 1, f) == 1) idx.push_back(v);
+    std::fclose(f);
+    for (int64_t p : idx)
+        if (p < 0 || p >= (int64_t)W * H) throw std::runtime_error("pixel index out of range");
+    Scene s = parse_scene_gltf(argv[2], W, H, spp);
+    const size_t n = idx.size();
+    std::vector<float> out(n * 3);
+    std::vector<uint64_t> pc(n * 6);
+    reset_counters();
+    double t0 = now_s();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+    for (size_t k = 0; k < n; ++k) {
+        const Counters before = cnt();
+        vector3f c = render_pixel(s, (int)(idx[k] % W), (int)(idx[k] / W), spp);
+        const Counters &after = cnt();
+        out[3 * k + 0] = c.x;
+        out[3 * k + 1] = c.y;
+        out[3 * k + 2] = c.z;
+        const uint64_t d[6] = {after.rays - before.rays, after.aabb - before.aabb, after.tri - before.tri,
+                               after.lqueries - before.lqueries, after.laabb - before.laabb, after.ltri - before.ltri};
+        std::memcpy(&pc[6 * k], d, sizeof d);
+    }
+    double t1 = now_s();
+    RtDump d(argv[7]);
+    d.put("index", idx);
+    d.put("sums", out, {(uint64_t)n, 3});
+    d.put("pixel_counters", pc, {(uint64_t)n, 6});
+    d.scalar<int32_t>("width", W);
+    d.scalar<int32_t>("height", H);
+    d.scalar<int32_t>("spp", spp);
+    d.close();
+    char extra[96];
+    std::snprintf(extra, sizeof extra, ", \"pixels\": %zu, \"spp\": %d", n, spp);
+    print_counts("pixels", total_counters(), t1 - t0, threads, extra);
     return 0;
 }
 
@@ -488,7 +539,7 @@ static int mode_finish(int argc, char **argv) {
 
 int main(int argc, char **argv) {
     try {
-        if (argc < 2) throw std::runtime_error("usage: ref_harness sums|time|rays|dump|samplers|finish ...");
+        if (argc < 2) throw std::runtime_error("usage: ref_harness sums|time|rays|dump|samplers|finish|pixels ...");
         std::string m = argv[1];
         if (m == "sums") return mode_sums(argc, argv);
         if (m == "time") return mode_time(argc, argv);
@@ -496,6 +547,7 @@ int main(int argc, char **argv) {
         if (m == "dump") return mode_dump(argc, argv);
         if (m == "samplers") return mode_samplers(argc, argv);
         if (m == "finish") return mode_finish(argc, argv);
+        if (m == "pixels") return mode_pixels(argc, argv);
         throw std::runtime_error("unknown mode " + m);
     } catch (const std::exception &e) {
         std::fprintf(stderr, "ref_harness: %s\n", e.what());

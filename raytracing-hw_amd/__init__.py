@@ -44,15 +44,19 @@ class RtSceneView(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 2          # include/rt_hw.h RT_ABI_VERSION
+ABI_VERSION = 3          # include/rt_hw.h RT_ABI_VERSION
+KERNEL_LANE = 0          # RT_KERNEL_LANE: lane-resident persistent kernel (default)
+KERNEL_WAVEFRONT = 4     # RT_KERNEL_WAVEFRONT: init / extend / shade launches
 FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES
 FLAG_FAST = 2            # RT_FLAG_FAST: per-(pixel, sample) Philox-seeded streams, not bit-identical to the reference
+FLAG_LIGHT_SPLIT = 4     # RT_FLAG_LIGHT_SPLIT: light-pdf walk as its own traversal state (same bits)
+FLAG_NATURAL_ORDER = 8   # RT_FLAG_NATURAL_ORDER: row-major pixel order instead of the in-frame heaviest-first order
 
 
 class RtParams(ctypes.Structure):
     _fields_ = [("spp", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
                 ("row_block", ctypes.c_int32), ("count", ctypes.c_int32), ("kernel", ctypes.c_int32),
-                ("flags", ctypes.c_int32), ("fast_chunk", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("fast_chunk", ctypes.c_int32), ("device", ctypes.c_int32)]
 
 
 class RtStats(ctypes.Structure):
@@ -60,7 +64,8 @@ class RtStats(ctypes.Structure):
                 ("aabb_tests", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("light_queries", ctypes.c_uint64),
                 ("light_aabb_tests", ctypes.c_uint64), ("light_tri_tests", ctypes.c_uint64), ("shading_hits", ctypes.c_uint64),
                 ("render_ms", ctypes.c_double), ("extend_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
-                ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64), ("extend_rays", ctypes.c_uint64)]
+                ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64), ("extend_rays", ctypes.c_uint64),
+                ("order_ms", ctypes.c_double), ("gather_ms", ctypes.c_double), ("devices", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -78,6 +83,8 @@ ABI = {
     "rt_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RtParams), _c_f, ctypes.POINTER(RtStats)]),
     "rt_render_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RtParams), ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.POINTER(RtStats)]),
+    "rt_render_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RtParams), ctypes.c_int32, _c_f,
+                                       ctypes.POINTER(RtStats)]),
     "rt_intersect_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_f, _c_f, _c_f,
                                          ctypes.POINTER(ctypes.c_int64)]),
     "rt_tonemap_u8": (ctypes.c_int, [_c_f, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _c_b]),
@@ -204,29 +211,43 @@ class Scene:
     def upload(self, device=0):
         _check(lib().rt_scene_upload(self._h, device))
 
-    def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False, fast=False, fast_chunk=0):
-        flags = (FLAG_KERNEL_TIMES if kernel_times else 0) | (FLAG_FAST if fast else 0)
-        return RtParams(spp or 0, rank, world, row_block, int(count), kernel, flags, fast_chunk)
+    def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False, fast=False, fast_chunk=0,
+                device=0, light_split=False, natural_order=False):
+        flags = ((FLAG_KERNEL_TIMES if kernel_times else 0) | (FLAG_FAST if fast else 0) |
+                 (FLAG_LIGHT_SPLIT if light_split else 0) | (FLAG_NATURAL_ORDER if natural_order else 0))
+        return RtParams(spp or 0, rank, world, row_block, int(count), kernel, flags, fast_chunk, device)
 
     def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0, fast=False,
-                    fast_chunk=0):
+                    fast_chunk=0, light_split=False, natural_order=False):
         """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42).
         fast=True: fast mode (RT_FLAG_FAST, work units of fast_chunk samples): statistically
-        equivalent to the reference, not bit-identical."""
-        self.upload(device)
+        equivalent to the reference, not bit-identical.  light_split / natural_order: other
+        schedules of the same bits (RT_FLAG_LIGHT_SPLIT, RT_FLAG_NATURAL_ORDER)."""
         rows = shard_rows(self.height, rank, world, row_block)
         out = np.zeros((len(rows), self.width, 3), np.float32)
         st = RtStats()
-        p = self._params(spp, rank, world, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk)
+        p = self._params(spp, rank, world, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk, device=device,
+                         light_split=light_split, natural_order=natural_order)
         _check(lib().rt_render(self._h, ctypes.byref(p), out.ctypes.data_as(_c_f), ctypes.byref(st)))
         return out, st.as_dict()
 
+    def render_multi(self, spp=None, n_devices=0, row_block=8, count=False, kernel=0, fast=False, fast_chunk=0):
+        """The whole frame over devices 0..n_devices-1 (0 = all visible; rt_render_multi):
+        one host thread per device, each rendering its row-block shard; (H, W, 3) sums."""
+        out = np.zeros((self.height, self.width, 3), np.float32)
+        st = RtStats()
+        p = self._params(spp, 0, 1, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk)
+        _check(lib().rt_render_multi(self._h, ctypes.byref(p), n_devices, out.ctypes.data_as(_c_f), ctypes.byref(st)))
+        return out, st.as_dict()
+
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
-                      kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0):
-        """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream.
-        kernel_times: per-launch HIP-event timing of the wavefront kernels (needs stats).
-        fast: fast mode (RT_FLAG_FAST), see render_sums."""
-        p = self._params(spp, rank, world, row_block, count, kernel, kernel_times, fast, fast_chunk)
+                      kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0, device=0,
+                      light_split=False, natural_order=False):
+        """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream, on
+        `device` (upload(device) first).  kernel_times: per-launch HIP-event timing of the
+        wavefront kernels (needs stats).  fast: fast mode (RT_FLAG_FAST), see render_sums."""
+        p = self._params(spp, rank, world, row_block, count, kernel, kernel_times, fast, fast_chunk, device,
+                         light_split, natural_order)
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))

@@ -4,20 +4,12 @@
 // 8 words per node: min.xyz, max.xyz, a, b (internal: a = left child, right = a + 1,
 // b = split axis < 3; leaf: a = first triangle, b = count << 2 | 3).
 //
-//   bfs_nodes   same records renumbered breadth-first: siblings stay adjacent, the top
-//               levels become a prefix (rt_wavefront.h LdsNodes), and the children pairs of
-//               two sibling internal nodes are adjacent pairs (used by wide_nodes).
-//   wide_nodes  the breadth-first records with the two index words repacked so that a
-//               node also says where its near child's children are (rt_trav_wide.h):
-//                 word 6  ab = a << 10 | b              (the node itself, one word)
-//                 word 7  c  = g << 2 | R internal << 1 | L internal
-//               g = the child pair of the first internal child among (L, R); by the
-//               breadth-first order the right child's pair is g + 2 when both are internal.
+//   bfs_nodes   same records renumbered breadth-first: siblings stay adjacent and the top
+//               levels become a prefix (the levels nearly every ray visits share lines).
 // Visits, counters and results do not depend on node numbering.
 #pragma once
 #include <cstdint>
 #include <cstring>
-#include <stdexcept>
 #include <vector>
 
 namespace rtd {
@@ -53,29 +45,6 @@ inline std::vector<float> bfs_nodes(const std::vector<float> &node) {
             const uint32_t na = new_id[node_word(node, u, 6)];
             std::memcpy(&out[8 * k + 6], &na, 4);
         }
-    }
-    return out;
-}
-
-// `bfs` must come from bfs_nodes.  Throws std::length_error past the packing limits
-// (2^22 nodes / triangles, 255 triangles per leaf: the same limits as the 8-byte frames).
-inline std::vector<float> wide_nodes(const std::vector<float> &bfs) {
-    const size_t n = bfs.size() / 8;
-    std::vector<float> out(bfs);
-    for (size_t k = 0; k < n; ++k) {
-        const uint32_t a = node_word(bfs, k, 6), b = node_word(bfs, k, 7);
-        if (a >= (1u << 22) || b >= 1024u) throw std::length_error("wide_nodes: BVH exceeds the 22/10-bit packing");
-        const uint32_t ab = a << 10 | b;
-        uint32_t c = 0;
-        if (b < 3u) {
-            const bool li = node_word(bfs, a, 7) < 3u, ri = node_word(bfs, a + 1, 7) < 3u;
-            const uint32_t gl = li ? node_word(bfs, a, 6) : 0u, gr = ri ? node_word(bfs, a + 1, 6) : 0u;
-            if (li && ri && gr != gl + 2) throw std::logic_error("wide_nodes: children pairs not adjacent");
-            const uint32_t g = li ? gl : gr;
-            c = g << 2 | (ri ? 2u : 0u) | (li ? 1u : 0u);
-        }
-        std::memcpy(&out[8 * k + 6], &ab, 4);
-        std::memcpy(&out[8 * k + 7], &c, 4);
     }
     return out;
 }

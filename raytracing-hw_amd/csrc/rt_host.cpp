@@ -151,6 +151,25 @@ V4 m4_mul_v4(const M4 &m, V4 t) {
 }
 V3 m4_mul_point(const M4 &m, V3 p) { return rtv::reduce(m4_mul_v4(m, {p.x, p.y, p.z, 1.f})); }
 V3 m4_mul_vector(const M4 &m, V3 p) { return rtv::reduce(m4_mul_v4(m, {p.x, p.y, p.z, 0.f})); }
+
+// The same products as the shipped reference binary computes them inside parse_scene_gltf's
+// triangle loop (scene_parser.cpp:300-319).  GCC 11 at -O3 (the reference's CMake build)
+// SLP-vectorizes that loop and keeps some of multiply()'s float accumulators in double, so a
+// component is rounded to float once, after all four products are added, instead of after
+// every add (matrix.h:66-72).  Determined against the reference's own dumps built with and
+// without -fno-tree-slp-vectorize (oracle/Makefile ref_harness_noslp, tests/test_loader.py):
+//   positions:  v0 and v1 - v0 as the source says; v2 - v0 in y and z from once-rounded
+//               v2 and v0 (x as the source says);
+//   normals:    multiplyVector(normal_transform, n) with x and y rounded once, z per add.
+// Meshes whose transforms make every product exact (identity, scale, axis swaps) are the
+// same either way.
+float m4_dot_once(const M4 &m, int i, V3 p, float w) {
+    return (float)(m.d[i] * (double)p.x + m.d[4 + i] * (double)p.y + m.d[8 + i] * (double)p.z + m.d[12 + i] * (double)w);
+}
+V3 m4_mul_vector_gcc(const M4 &m, V3 p) {
+    const V3 r = m4_mul_vector(m, p);
+    return {m4_dot_once(m, 0, p, 0.f), m4_dot_once(m, 1, p, 0.f), r.z};
+}
 M4 m4_transpose(const M4 &m) {
     M4 r;
     for (int i = 0; i < 4; ++i)
@@ -587,16 +606,20 @@ static void load_gltf(rt_scene &S, const std::string &path, int width, int heigh
                                                      : ((const uint32_t *)iv.data)[t * 3 + v];
                 Prim pr;
                 pr.mesh_id = mesh_id;
+                V3 q[3];
                 for (int v = 0; v < 3; ++v) {
-                    V3 q{pos_v[index[v] * 3], pos_v[index[v] * 3 + 1], pos_v[index[v] * 3 + 2]};
-                    pr.pos[v] = m4_mul_point(transform, q);
+                    q[v] = V3{pos_v[index[v] * 3], pos_v[index[v] * 3 + 1], pos_v[index[v] * 3 + 2]};
+                    pr.pos[v] = m4_mul_point(transform, q[v]);
                 }
+                // (the reference binary's v2 - v0: see m4_mul_vector_gcc)
+                const float y0 = m4_dot_once(transform, 1, q[0], 1.f), z0 = m4_dot_once(transform, 2, q[0], 1.f);
+                const float y2 = m4_dot_once(transform, 1, q[2], 1.f), z2 = m4_dot_once(transform, 2, q[2], 1.f);
                 pr.pos[1] = rtv::sub(pr.pos[1], pr.pos[0]);
-                pr.pos[2] = rtv::sub(pr.pos[2], pr.pos[0]);
+                pr.pos[2] = V3{pr.pos[2].x - pr.pos[0].x, y2 - y0, z2 - z0};
                 for (int v = 0; v < 3; ++v) {
                     V3 n = nrm_v ? V3{nrm_v[index[v] * 3], nrm_v[index[v] * 3 + 1], nrm_v[index[v] * 3 + 2]}
                                  : V3{0.f, 0.f, 1.f};
-                    pr.nrm[v] = rtv::normal(m4_mul_vector(mesh.normal_transform, n));
+                    pr.nrm[v] = rtv::normal(m4_mul_vector_gcc(mesh.normal_transform, n));
                 }
                 for (int v = 0; v < 3; ++v) {
                     pr.tc[v] = tc_v ? V2{tc_v[index[v] * 2], tc_v[index[v] * 2 + 1]} : V2{0.f, 0.f};

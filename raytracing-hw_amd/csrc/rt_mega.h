@@ -17,32 +17,6 @@
 // to memory (LaneRec, indexed by lane slot).  Same per-pixel arithmetic, so bit-identical output.
 #pragma once
 #include "rt_wavefront.h"
-#include "rt_trav_wide.h"
-#include "rt_team.h"
-
-// RT_TEAM: a wave down to one traversing pixel walks that ray with all its lanes (rt_team.h).
-// Bit-exact (GPU parity tests), but measured on sponza 1080p x256spp: a team ray costs ~84 k
-// cycles against ~46 steps x 3-6 k cycles for a lane alone, yet the frame is no faster at 1
-// or 8 GPUs (a wave is rarely down to one pixel for long: the spread order puts pixels of
-// similar cost in every wave), and compiling the path in costs 7% (register allocation of
-// the main loop).  Off.
-#ifndef RT_TEAM
-#define RT_TEAM 0
-#endif
-
-// RT_WIDE: traversal by trav_step_w (rt_trav_wide.h: two node levels or two triangles per
-// iteration, from the wide node array) instead of trav_step (one unit per iteration).
-// Measured on sponza 1080p x256spp: both levels 1179 vs 1380 Mrays/s at 1 GPU;
-// the triangle pair alone 1294 at 1 GPU, 4% faster on an 8-way shard.  The loop is bound by
-// VALU issue, not by the number of dependent round trips, so the default stays off.
-#ifndef RT_WIDE
-#define RT_WIDE 0
-#endif
-
-// RT_LANE_RECORDS: vertex records by lane slot (LaneRec) instead of by pixel (AosRec).
-#ifndef RT_LANE_RECORDS
-#define RT_LANE_RECORDS 1
-#endif
 
 namespace rtd {
 
@@ -54,14 +28,8 @@ inline thread_local long long g_mega_slot = 0;
 inline long long mega_slot() { return g_mega_slot; }
 #endif
 
-#if RT_WIDE
-using MegaTrav = TravW;
-// the root record as mega_begin reads it: load_node(sc.node_w, 0) (a = ab word, b = c word)
-__device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return sc.node_w; }
-#else
 using MegaTrav = TravState;
 __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return sc.node; }
-#endif
 
 // M_LTRAV / M_LREADY: light-pdf walk as its own traversal (light-split kernel, below)
 enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4 };
@@ -75,20 +43,17 @@ struct MegaLane {
     int send;
     uint32_t gpix;
     long long dst;
-    unsigned long long work0;   // counting runs: traversal tests before this pixel (pixel cost)
+    unsigned long long work0;   // counting runs: traversal tests before this work unit (its cost)
     Rng rng;
     V3 sum;
     Ray r;
     MegaTrav T;
 };
 
-// RT_MEGA_LDS_SUM: the lane's pixel sum lives in LDS (3 KB per block) instead of three VGPRs
-// that stay live through the shading code.  With RT_MEGA_LDS_RNG: 30 -> 17 spilled VGPRs at
+// The lane's pixel sum lives in LDS (3 KB per block) instead of three VGPRs that stay live
+// through the shading code; with the RNG state below in LDS too: 30 -> 17 spilled VGPRs at
 // the 96-VGPR budget, 1478 -> 1517 Mrays/s at 1080p x256spp, 8-way shard 325 -> 318 ms.
-#ifndef RT_MEGA_LDS_SUM
-#define RT_MEGA_LDS_SUM 1
-#endif
-#if RT_MEGA_LDS_SUM && defined(__HIPCC__)
+#if defined(__HIPCC__)
 __shared__ float mega_lds_sum[3 * 256];
 __device__ __forceinline__ V3 lane_sum(const MegaLane &) {
     const int t = threadIdx.x;
@@ -105,13 +70,9 @@ __device__ __forceinline__ V3 lane_sum(const MegaLane &L) { return L.sum; }
 __device__ __forceinline__ void lane_sum_set(MegaLane &L, V3 v) { L.sum = v; }
 #endif
 
-// RT_MEGA_LDS_RNG: the lane's RNG state (minstd word, normal cache) lives in LDS between
-// its uses (sample start, shading), 3 KB per block, instead of three VGPRs held through the
-// traversal.
-#ifndef RT_MEGA_LDS_RNG
-#define RT_MEGA_LDS_RNG 1
-#endif
-#if RT_MEGA_LDS_RNG && defined(__HIPCC__)
+// The lane's RNG state (minstd word, normal cache) lives in LDS between its uses (sample
+// start, shading), 3 KB per block, instead of three VGPRs held through the traversal.
+#if defined(__HIPCC__)
 __shared__ uint32_t mega_lds_rng[3 * 256];
 __device__ __forceinline__ Rng lane_rng(const MegaLane &) {
     const int t = threadIdx.x;
@@ -128,54 +89,16 @@ __device__ __forceinline__ Rng lane_rng(const MegaLane &L) { return L.rng; }
 __device__ __forceinline__ void lane_rng_set(MegaLane &L, const Rng &r) { L.rng = r; }
 #endif
 
-// RT_MEGA_LDS_CTR: the lane's sample counter, depth budget and recorded-vertex count live in
-// LDS (3 KB per block); shading loads them once and stores them back (A/B knob).
-#ifndef RT_MEGA_LDS_CTR
-#define RT_MEGA_LDS_CTR 0
-#endif
+// The lane's sample counter, depth budget and recorded-vertex count (registers; measured
+// no faster in LDS).
 struct LaneCtr {
     int s, power, nv;
 };
-#if RT_MEGA_LDS_CTR && defined(__HIPCC__)
-__shared__ int mega_lds_ctr[3 * 256];
-__device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &) {
-    const int t = threadIdx.x;
-    return LaneCtr{mega_lds_ctr[t], mega_lds_ctr[256 + t], mega_lds_ctr[512 + t]};
-}
-__device__ __forceinline__ void lane_ctr_set(MegaLane &, const LaneCtr &c) {
-    const int t = threadIdx.x;
-    mega_lds_ctr[t] = c.s;
-    mega_lds_ctr[256 + t] = c.power;
-    mega_lds_ctr[512 + t] = c.nv;
-}
-#else
 __device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &L) { return LaneCtr{L.s, L.power, L.nv}; }
 __device__ __forceinline__ void lane_ctr_set(MegaLane &L, const LaneCtr &c) {
     L.s = c.s;
     L.power = c.power;
     L.nv = c.nv;
-}
-#endif
-
-// RT_MEGA_UV_RECOMPUTE: shading recomputes the winner's barycentrics (the traversal's own
-// tri_hit_bl on the same ray and triangle: the same bits), so TravState's best.u / best.v
-// are never read and the traversal stops carrying them (A/B knob).
-#ifndef RT_MEGA_UV_RECOMPUTE
-#define RT_MEGA_UV_RECOMPUTE 0
-#endif
-__device__ __forceinline__ Hit mega_best(const MegaLane &L, const DevScene &sc) {
-    Hit h = L.T.best;
-#if RT_MEGA_UV_RECOMPUTE
-    if (h.prim >= 0) {
-        const float4 *q = sc.tri + 3 * (size_t)h.prim;
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-        TriHit th;
-        tri_hit_bl(V3{q0.x, q0.y, q0.z}, V3{q0.w, q1.x, q1.y}, V3{q1.z, q1.w, q2.x}, L.r, th);
-        h.u = th.u;
-        h.v = th.v;
-    }
-#endif
-    return h;
 }
 
 // Closest-hit query start for L.r: BVH::intersect's counters and root box (bvh.cpp:239-243).
@@ -184,11 +107,7 @@ __device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Cou
     float e;
     const bool hit = box_hit<false>(root.mn, root.mx, L.r, e);
     const uint32_t bits = (L.r.d.x > 0 ? 1u : 0u) | (L.r.d.y > 0 ? 2u : 0u) | (L.r.d.z > 0 ? 4u : 0u) | (hit ? 0u : 8u);
-#if RT_WIDE
-    L.state = trav_start_w<COUNT>(bits, root.a, root.b, L.T, cnt) ? M_TRAV : M_READY;
-#else
     L.state = trav_start<COUNT>(bits, root.a, root.b, L.T, cnt) ? M_TRAV : M_READY;
-#endif
 }
 
 // Next sample of the lane's pixel: jittered camera ray (scene.cpp:36-39).  Fast mode: the
@@ -239,6 +158,7 @@ __device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc
     lane_ctr_set(L, LaneCtr{s0, 0, 0});
     L.send = s0 + cs < spp ? s0 + cs : spp;
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
+    L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
     const int k = p / g.width, px = p - k * g.width, py = shard_row(g, k);
     L.gpix = (uint32_t)(py * sc.width + px);
     mega_sample<COUNT, true>(L, sc, g, root, cnt);
@@ -249,12 +169,8 @@ __device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc
 template <bool COUNT, bool FAST = false>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Counters &cnt) {
-#if RT_LANE_RECORDS
     LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
-#else
-    AosRec P{st.rec_ab, st.rec_c, L.pix, st.D, V3{0.f, 0.f, 0.f}, 0, false};
-#endif
-    const Hit h = mega_best(L, sc);
+    const Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
     bool next = false;
     if (h.prim >= 0 && h.t < sc.max_distance) {
@@ -279,7 +195,7 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
         out[3 * o + 0] = sm.x;
         out[3 * o + 1] = sm.y;
         out[3 * o + 2] = sm.z;
-        if (COUNT && !FAST && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
+        if (COUNT && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
         L.pix = -1;
         L.state = M_IDLE;
         return;
@@ -352,7 +268,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
     LaneCtr c = lane_ctr(L);
     bool next = false;
     if (L.state == M_READY) {
-        const Hit h = mega_best(L, sc);
+        const Hit h = L.T.best;
         ShadeMid m;
         bool pre = false;
         if (h.prim >= 0 && h.t < sc.max_distance) {
@@ -409,7 +325,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
         out[3 * o + 0] = sm.x;
         out[3 * o + 1] = sm.y;
         out[3 * o + 2] = sm.z;
-        if (COUNT && !FAST && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
+        if (COUNT && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
         L.pix = -1;
         L.state = M_IDLE;
         return;
@@ -418,46 +334,13 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
     mega_sample<COUNT, FAST>(L, sc, g, root, cnt);
 }
 
-#if RT_TEAM && defined(__HIPCC__) && !RT_WIDE
-// The rest of lane `owner`'s ray by the whole wave (trav_team); false if its frames are not
-// all in LDS.  Then the owner is READY, as after its last trav_step.
-__device__ __forceinline__ bool mega_team(MegaLane &L, int owner, const DevScene &sc) {
-    const int lane = threadIdx.x & 63;
-    const int sp = (int)team_u((uint32_t)L.T.sp, owner);
-    if (sp > kLdsStack) return false;
-    Ray r;
-    r.o = V3{team_f(L.r.o.x, owner), team_f(L.r.o.y, owner), team_f(L.r.o.z, owner)};
-    r.d = V3{team_f(L.r.d.x, owner), team_f(L.r.d.y, owner), team_f(L.r.d.z, owner)};
-    r.inv = V3{team_f(L.r.inv.x, owner), team_f(L.r.inv.y, owner), team_f(L.r.inv.z, owner)};
-    TravState T;
-    T.a = team_u(L.T.a, owner);
-    T.b = team_u(L.T.b, owner);
-    T.k = team_u(L.T.k, owner);
-    T.kend = team_u(L.T.kend, owner);
-    T.acc = team_f(L.T.acc, owner);
-    T.sp = sp;
-    T.phase = (int)team_u((uint32_t)L.T.phase, owner);
-    T.best.t = team_f(L.T.best.t, owner);
-    T.best.u = team_f(L.T.best.u, owner);
-    T.best.v = team_f(L.T.best.v, owner);
-    T.best.prim = (int)team_u((uint32_t)L.T.best.prim, owner);
-    const TeamStack stk{(int)(threadIdx.x & ~63u), owner};
-    trav_team(sc, r, T, stk, lane);
-    if (lane == owner) {
-        L.T = T;
-        L.state = M_READY;
-    }
-    return true;
-}
-#endif
-
 // One iteration of a wave's main loop for one lane, given the wave's decision: shade the
 // READY lanes this iteration (shade_now), or step the traversing lanes.
 template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT = false>
 __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
                                              const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt) {
-    if constexpr (LSPLIT) {   // (not with RT_WIDE: the light walk uses TravState and the pair stack)
+    if constexpr (LSPLIT) {
         if (shade_now) {
             if (L.state == M_READY || L.state == M_LREADY)
                 mega_shade_split<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt);
@@ -471,11 +354,7 @@ __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const 
     if (shade_now) {
         if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, cnt);
     } else if (L.state == M_TRAV) {
-#if RT_WIDE
-        if (trav_step_w<COUNT>(sc, L.r, L.T, stk, cnt)) L.state = M_READY;
-#else
         if (trav_step<COUNT>(sc, L.r, L.T, stk, nodes, cnt)) L.state = M_READY;
-#endif
     }
 }
 

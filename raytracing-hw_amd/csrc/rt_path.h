@@ -93,7 +93,6 @@ struct DevScene {
     const float4 *tri_attr;   // 4 x float4 / triangle: normals, texcoords, mesh id
     const float4 *tri_tan;    // 3 x float4 / triangle: tangents
     const float4 *node;       // 2 x float4 / node: (min, max.x) (max.yz, a, b)
-    const float4 *node_w;     // 2 x float4 / node, breadth-first: (min, max.x) (max.yz, ab, c) (rt_bvh_layout.h)
     const float4 *light;      // 4 x float4 / light triangle
     const float4 *light_node;
     const float *mesh_f;      // 12 / mesh

@@ -6,7 +6,10 @@
 
 #include "../../include/rt_hw.h"
 
-struct rt_device_scene;  // owned by rt_device.hip
+struct rt_device_scene;  // owned by rt_device.hip: one per device the scene is uploaded to
+struct rt_device_blob;   // owned by rt_device.hip: the device image of the scene, built once
+
+constexpr int kRtMaxDevices = 64;
 
 struct rt_scene {
     int32_t width = 0, height = 0, samples = 0, ray_depth = 6;
@@ -26,14 +29,15 @@ struct rt_scene {
     std::vector<uint32_t> tex_info;
     std::vector<uint8_t> texels;
 
-    rt_device_scene *dev = nullptr;
+    rt_device_scene *dev[kRtMaxDevices] = {};   // [HIP device id]
+    rt_device_blob *blob = nullptr;
 };
 
 // error plumbing shared by rt_host.cpp and rt_device.hip
 void rt_set_error(const std::string &msg);
 int rt_fail(int code, const std::string &msg);
 
-// implemented in rt_device.hip
+// implemented in rt_device.hip: frees every device copy and the device image
 void rt_device_scene_release(rt_scene *s);
 
 // row partition helper (rt_host.cpp)

@@ -14,9 +14,20 @@
 // bit-identical to the reference's per-pixel recursion.  Queues are compacted with one
 // atomic per wave (ballot + mbcnt ranks keep lane order).
 #pragma once
-#include "rt_wave.h"
+#include "rt_path.h"
 
 namespace rtd {
+
+// Pixel-row shard geometry (include/rt_hw.h rt_params): the k-th owned row of rank r is
+// the k-th row whose (row / row_block) % world == rank.
+struct ShardGeom {
+    int width, rank, world, row_block;
+    long long n_pixels;
+};
+__device__ __forceinline__ int shard_row(const ShardGeom &g, int k) {
+    const int blk = k / g.row_block;
+    return (blk * g.world + g.rank) * g.row_block + (k % g.row_block);
+}
 
 struct WfState {
     long long n;      // path slots (= pixels of the shard)
@@ -194,11 +205,6 @@ __device__ __forceinline__ void box_pair_hit(const NodeRec &L, const NodeRec &R,
     insideF = lf ? inR : inL;
 }
 
-// tri_hit_bl's 1 / det by rcp_ieee (compile-time A/B knob; 0 = the compiler's IEEE division).
-#ifndef RT_FAST_RCP
-#define RT_FAST_RCP 1
-#endif
-
 // 1.f / x, correctly rounded, in three instructions where that is exact: the hardware
 // reciprocal (about 1 ulp) and one fma Newton correction, which rounds correctly for every
 // normal x with a normal reciprocal — checked on the device over every such float
@@ -224,11 +230,7 @@ __device__ __forceinline__ bool tri_hit_bl(V3 v0, V3 U, V3 V, const Ray &r, TriH
     // -1e-6 < (double)det < 1e-6 in float: 0x1.0c6f7cp-20f is the least float above the double
     // 1e-6, so the double compares and |det| < it agree on every float (NaN included)
     const bool ok_det = !(__builtin_fabsf(det) < 0x1.0c6f7cp-20f);
-#if RT_FAST_RCP
     const float inv_det = rcp_ieee(det);
-#else
-    const float inv_det = 1.f / det;
-#endif
     const V3 s = rtv::sub(r.o, v0);
     const float u = inv_det * rtv::dot(s, p);
     const V3 q = rtv::cross(s, U);
@@ -284,29 +286,11 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
     q[kQRec * (size_t)p] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
 }
 
-// trav_step tests a child pair with box_pair_hit (compile-time A/B knob; 0 = box_hit_pt twice).
-#ifndef RT_BOX_PAIR
-#define RT_BOX_PAIR 1
-#endif
-// trav_step issues the node-pair and triangle reads together (compile-time A/B knob).
-#ifndef RT_HOIST_LOADS
-#define RT_HOIST_LOADS 1
-#endif
-// trav_step_n keeps a far child's squared entry distance and compares it with the exact
-// midpoint test (sqrt_gt) instead of taking a correctly rounded sqrt per node step.  Exact
-// (tests/test_kernel_host.py), but 5% slower on sponza 1080p at 1 GPU (double-precision
-// compares on every return); off.  (Choosing the near child by selecting dir[split axis]
-// instead of the sign-bit mask was tried too: 1.6x slower — the register allocation of the
-// whole loop changed.)
-#ifndef RT_SQ_CULL
-#define RT_SQ_CULL 0
-#endif
-// Leaf triangles tested per trav_step (1-4; node arrays in plain memory only).  A node lane
-// and a leaf lane read through the same registers: 4 x 16 B of the child pair, or of
-// triangle k (its 3 x 16 B and the next record's first), then 3 x 16 B per further triangle.
-// Sponza 1080p x256spp, lane-resident kernel: 2 is +3.6% at 1 GPU and -7% on the rank-0
-// shard of an 8-way split (fewer iterations on the heaviest pixel's chain); 3 and 4 lose
-// at 1 GPU (more registers live across the step).
+// Leaf triangles tested per traversal step.  A node lane and a leaf lane read through the
+// same registers: 4 x 16 B of the child pair, or of triangle k (its 3 x 16 B and the next
+// record's first), then 3 x 16 B per further triangle.  Sponza 1080p x256spp, lane-resident
+// kernel: 2 is +3.6% at 1 GPU over 1 and -7% on the rank-0 shard of an 8-way split; 3 and 4
+// lose at 1 GPU (more registers live across the step).  (Host tests build other values.)
 #ifndef RT_LEAF_N
 #define RT_LEAF_N 2
 #endif
@@ -322,10 +306,8 @@ struct TravState {
     Hit best;        // global winner so far (strict <, first of equal t wins)
 };
 
-// Where trav_step reads child pairs from: the node array in HBM ...
+// Where trav_step reads child pairs from: the breadth-first node array in HBM.
 struct GlobalNodes {
-    static constexpr bool kPtr = true;   // pairs are plain memory (trav_step's shared load registers)
-    static constexpr bool kLdsTop = false;
     const float4 *node;
     __device__ __forceinline__ const float4 *pair(uint32_t left) const { return node + 2 * (size_t)left; }
     __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
@@ -366,18 +348,6 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
     return (bits & 8u) == 0;
 }
 
-// sqrtf(x) > a, correctly rounded sqrt, without the sqrt: for a > 0 with next float n,
-// sqrtf(x) > a iff sqrt(x) > (a + n) / 2 (a tie is impossible: (a + n)^2 / 4 is an odd
-// square of ulps, far wider than a float), i.e. 4x > (a + n)^2, both sides exact in double.
-// For a = +-0: sqrtf(x) > 0 iff x > 0.  NaN x: false, as the comparison it replaces.  x is a
-// squared length (>= 0 or NaN) and a a hit distance or the local best (>= 0, finite).
-__device__ __forceinline__ bool sqrt_gt(float x, float a) {
-    if (!(a > 0.f)) return x > 0.f;
-    const float n = __uint_as_float(__float_as_uint(a) + 1u);
-    const double m = (double)a + (double)n;
-    return 4.0 * (double)x > m * m;
-}
-
 // The return of trav_step: merge subtree bests upwards until a far child is to be visited
 // (enter it: false) or the stack is empty (T.best is final: true).
 template <class Stack>
@@ -396,11 +366,7 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
             acc = acc < p ? acc : p;
             continue;
         }
-#if RT_SQ_CULL
-        if (!sqrt_gt(__uint_as_float(f.y), acc)) {   // far child survives the near subtree's best
-#else
         if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
-#endif
             stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
 #ifdef RT_STACK_PROBE
             RT_STACK_PROBE(sp);
@@ -413,30 +379,28 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
     }
 }
 
-// trav_step with RT_LEAF_N triangles per leaf step (see RT_LEAF_N).  Same node step, same
-// frames; a leaf lane tests triangles k .. k + N - 1 of its leaf in the reference's order
-// (strict <, so the first of equal t wins), which is the sequence of N single steps.
+// One unit of traversal work: the child pair of one internal node, or RT_LEAF_N triangles
+// of a leaf, followed (when the subtree is finished) by the return up the frames until a
+// far child is to be visited.  Returns true once the stack is empty (T.best is final).  A
+// wave's lanes each advance by one unit per call, whatever mix of units they are at.
+// A leaf lane tests triangles k .. k + N - 1 in the reference's order (strict <, so the
+// first of equal t wins), which is the sequence of N single-triangle steps.
+// Both memory reads of the step issue before either test (node lanes and leaf lanes load
+// through the same registers), so a wave split between node and leaf steps waits for one
+// round trip per iteration, not two.
 template <bool COUNT, class Stack, class Nodes>
-__device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
-                                            const Nodes &nodes, Counters &cnt, bool at_node, bool at_leaf) {
+__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
+                                          const Nodes &nodes, Counters &cnt) {
     constexpr int N = RT_LEAF_N;
+    const bool at_node = T.phase == TP_NODE, at_leaf = T.phase == TP_LEAF;
     const uint32_t k = T.k, klast = T.kend - 1u;
     RT_CHECK(!at_node || T.a + 1 < (uint32_t)sc.n_nodes, 10, T.a, T.a = 0);
     RT_CHECK(!at_leaf || T.kend <= (uint32_t)sc.n_tris, 12, T.kend, T.k = T.kend = 1);
     float4 q[4 + 3 * (N - 1)];
     {
-        bool from_lds = false;
-        if constexpr (Nodes::kLdsTop) from_lds = at_node && Nodes::in_lds(T.a);
-        if (from_lds) {
-            if constexpr (Nodes::kLdsTop) {
+        const float4 *p0 = at_node ? nodes.pair(T.a) : sc.tri + 3 * (size_t)(at_leaf ? k : 0u);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) q[i] = Nodes::lds(T.a, i);
-            }
-        } else {
-            const float4 *p0 = at_node ? nodes.pair(T.a) : sc.tri + 3 * (size_t)(at_leaf ? k : 0u);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) q[i] = p0[i];
-        }
+        for (int i = 0; i < 4; ++i) q[i] = p0[i];
 #pragma unroll
         for (int j = 1; j < N; ++j) {
             const uint32_t kj = at_leaf ? (k + j < klast ? k + j : klast) : 0u;
@@ -445,6 +409,7 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
             for (int i = 0; i < 3; ++i) q[4 + 3 * (j - 1) + i] = pj[i];
         }
 #ifdef __HIPCC__
+        // (pin the loads here: otherwise the compiler sinks each into its own branch again)
         asm volatile("" ::"v"(q[0].x), "v"(q[1].y), "v"(q[2].z), "v"(q[3].w));
 #endif
     }
@@ -455,20 +420,14 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
         R.mn[0] = q[2].x; R.mn[1] = q[2].y; R.mn[2] = q[2].z; R.mx[0] = q[2].w; R.mx[1] = q[3].x; R.mx[2] = q[3].y;
         R.a = __float_as_uint(q[3].z); R.b = __float_as_uint(q[3].w);
         if (COUNT) cnt.aabb += 2;
+        // dir[split axis] > 0: left child first (sign bits recomputed: cheaper than a register)
         const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
         const bool lf = (dpos >> T.b) & 1u;
+        // test both boxes as they are stored, then name them near / far
         float cF[3];
         bool hL, hR, inF;
         box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
-#if RT_SQ_CULL
-        // the far child's squared entry distance (box_dist before its sqrt; 0 from inside)
-        const V3 dF = rtv::sub(V3{cF[0], cF[1], cF[2]}, r.o);
-        const float ef = inF ? 0.f : rtv::dot(dF, dF);
-        const bool ef_gt_1e9 = sqrt_gt(ef, 1e9f);
-#else
-        const float ef = box_dist(cF, inF, r);
-        const bool ef_gt_1e9 = ef > 1e9f;
-#endif
+        const float ef = box_dist(cF, inF, r);   // the far child's entry distance
         const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
         const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
         if (hn && hf) {
@@ -478,7 +437,9 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
             RT_STACK_PROBE(T.sp);
 #endif
         }
-        const bool far_only = !hn && hf && !ef_gt_1e9;
+        // near child; or, the near box missed, the far child unless its entry distance
+        // exceeds the node's local best (still 1e9); or return
+        const bool far_only = !hn && hf && !(ef > 1e9f);
         if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
         else T.phase = TP_POP;
     } else if (at_leaf) {
@@ -499,115 +460,6 @@ __device__ __forceinline__ bool trav_step_n(const DevScene &sc, const Ray &r, Tr
         if (T.k >= T.kend) T.phase = TP_POP;
     }
     if (T.phase == TP_POP) return trav_pop(T, stk);
-    return false;
-}
-
-// One unit of traversal work: the child pair of one internal node, or one leaf triangle,
-// followed (when the subtree is finished) by the return up the frames until a far child
-// is to be visited.  Returns true once the stack is empty (T.best is final).  A wave's
-// lanes each advance by one unit per call, whatever mix of units they are at.
-template <bool COUNT, class Stack, class Nodes>
-__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, const Nodes &nodes,
-                                          Counters &cnt) {
-    const bool at_node = T.phase == TP_NODE, at_leaf = T.phase == TP_LEAF;
-    if constexpr (RT_LEAF_N > 1 && (Nodes::kPtr || Nodes::kLdsTop)) return trav_step_n<COUNT>(sc, r, T, stk, nodes, cnt, at_node, at_leaf);
-    NodeRec L, R;
-    V3 v0, U, V;
-#if RT_HOIST_LOADS
-    // Both memory reads of the step issue before either test: a wave whose lanes are split
-    // between node and leaf steps waits for one round trip per iteration, not two.  Lanes in
-    // the other phase read a fixed, cached address (pair 0 / triangle 0) and ignore it.
-    nodes.load_pair(at_node ? T.a : 0u, L, R);
-    load_tri(sc.tri, at_leaf ? (int)T.k : 0, v0, U, V);
-#ifdef __HIPCC__
-    // (pin the loads here: otherwise the compiler sinks each into its own branch again)
-    asm volatile("" ::"v"(L.mn[0]), "v"(L.mx[1]), "v"(R.mn[0]), "v"(R.mx[1]), "v"(v0.x), "v"(U.y), "v"(V.z));
-#endif
-#endif
-    if (at_node) {
-        const uint32_t a = T.a, b = T.b;
-        RT_CHECK(a + 1 < (uint32_t)sc.n_nodes, 10, a, T.a = 0);
-#if !RT_HOIST_LOADS
-        nodes.load_pair(a, L, R);
-#endif
-        if (COUNT) cnt.aabb += 2;
-        // dir[split axis] > 0: left child first (sign bits recomputed: cheaper than a register)
-        const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
-        const bool lf = (dpos >> b) & 1u;
-        // test both boxes as they are stored, then name them near / far
-        float cF[3];
-#if RT_BOX_PAIR
-        bool hL, hR, inF;
-        box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
-        const float ef = box_dist(cF, inF, r);   // the far child's entry distance
-#else
-        float cL[3], cR[3];
-        bool inL, inR;
-        const bool hL = box_hit_pt(L.mn, L.mx, r, cL, inL);
-        const bool hR = box_hit_pt(R.mn, R.mx, r, cR, inR);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) cF[k] = lf ? cR[k] : cL[k];
-        const float ef = box_dist(cF, lf ? inR : inL, r);   // the far child's entry distance
-#endif
-        const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
-        NodeRec N, F;
-        N.a = lf ? L.a : R.a; N.b = lf ? L.b : R.b;
-        F.a = lf ? R.a : L.a; F.b = lf ? R.b : L.b;
-        if (hn && hf) {
-            RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
-            stk.put(T.sp++, make_uint2((F.a << 10) | F.b, __float_as_uint(ef)));
-#ifdef RT_STACK_PROBE
-            RT_STACK_PROBE(T.sp);
-#endif
-        }
-        // near child; or, the near box missed, the far child unless its entry distance
-        // exceeds the node's local best (still 1e9); or return
-        const bool far_only = !hn && hf && !(ef > 1e9f);
-        if (hn || far_only) trav_enter(T, hn ? N.a : F.a, hn ? N.b : F.b);
-        else T.phase = TP_POP;
-    } else if (at_leaf) {
-        const uint32_t k = T.k;
-        RT_CHECK(k < (uint32_t)sc.n_tris, 12, k, T.k = 0);
-#if !RT_HOIST_LOADS
-        load_tri(sc.tri, (int)k, v0, U, V);
-#endif
-        TriHit h;
-        if (COUNT) cnt.tri++;
-        if (tri_hit_bl(v0, U, V, r, h)) {
-            T.acc = h.t < T.acc ? h.t : T.acc;
-            if (h.t < T.best.t) { T.best.t = h.t; T.best.u = h.u; T.best.v = h.v; T.best.prim = (int)k; }
-        }
-        T.k = k + 1;
-        if (T.k >= T.kend) T.phase = TP_POP;
-    }
-    if (T.phase == TP_POP) {
-        // return: merge subtree bests upwards until a far child is to be visited
-        float acc = T.acc;
-        int sp = T.sp;
-        for (;;) {
-            if (sp == 0) {
-                T.sp = 0;
-                T.acc = acc;
-                return true;
-            }
-            const uint2 f = stk.get(--sp);
-            if (f.x == kFrameAcc) {
-                const float p = __uint_as_float(f.y);
-                acc = acc < p ? acc : p;
-                continue;
-            }
-            if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
-                stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
-#ifdef RT_STACK_PROBE
-                RT_STACK_PROBE(sp);
-#endif
-                T.sp = sp;
-                T.acc = 1e9f;
-                trav_enter(T, f.x >> 10, f.x & 1023u);
-                return false;
-            }
-        }
-    }
     return false;
 }
 
@@ -640,42 +492,6 @@ struct LdsStack {
     }
 };
 
-// ... or, for the top of the tree, LDS.  The device node array is breadth-first
-// (rt_device.hip bfs_nodes), so its first kLdsNodes nodes are the top levels, which nearly
-// every ray visits; each block keeps a copy and reads those pairs with ds_read.
-#ifndef RT_LDS_NODES
-#define RT_LDS_NODES 128
-#endif
-constexpr int kLdsNodes = RT_LDS_NODES;   // 128: 4 KB, the top 7 levels of a full tree
-__shared__ float4 wf_lds_nodes[2 * kLdsNodes];
-struct LdsNodes {
-    static constexpr bool kPtr = false;
-    static constexpr bool kLdsTop = true;   // trav_step_n: pairs below kLdsNodes from LDS, the rest from `pair`
-    const float4 *node;
-    __device__ __forceinline__ const float4 *pair(uint32_t left) const { return node + 2 * (size_t)left; }
-    __device__ __forceinline__ static bool in_lds(uint32_t left) { return left + 1 < (uint32_t)kLdsNodes; }
-    __device__ __forceinline__ static float4 lds(uint32_t left, int i) { return wf_lds_nodes[2 * left + i]; }
-    __device__ __forceinline__ void load_pair(uint32_t left, NodeRec &L, NodeRec &R) const {
-        if (left + 1 < (uint32_t)kLdsNodes) {
-            const float4 p0 = wf_lds_nodes[2 * left], q0 = wf_lds_nodes[2 * left + 1];
-            const float4 p1 = wf_lds_nodes[2 * left + 2], q1 = wf_lds_nodes[2 * left + 3];
-            L.mn[0] = p0.x; L.mn[1] = p0.y; L.mn[2] = p0.z; L.mx[0] = p0.w; L.mx[1] = q0.x; L.mx[2] = q0.y;
-            L.a = __float_as_uint(q0.z); L.b = __float_as_uint(q0.w);
-            R.mn[0] = p1.x; R.mn[1] = p1.y; R.mn[2] = p1.z; R.mx[0] = p1.w; R.mx[1] = q1.x; R.mx[2] = q1.y;
-            R.a = __float_as_uint(q1.z); R.b = __float_as_uint(q1.w);
-        } else {
-            rtd::load_pair(node, left, L, R);
-            // keeps the two sources apart (merged, they become flat loads through a selected pointer)
-            asm volatile("" : "+v"(L.a), "+v"(R.a));
-        }
-    }
-    // block-cooperative fill; call before the first traversal, all threads of the block
-    __device__ __forceinline__ static void fill(const float4 *node, int n_nodes) {
-        const int m = 2 * (n_nodes < kLdsNodes ? n_nodes : kLdsNodes);
-        for (int k = threadIdx.x; k < m; k += blockDim.x) wf_lds_nodes[k] = node[k];
-        __syncthreads();
-    }
-};
 #endif
 
 // The whole closest-hit query through a queue record (host tests; the device kernel

@@ -15,13 +15,11 @@ static rtd::DevScene make(const rt_scene_view *v) {
     s.tri_attr = (const float4 *)v->tri_attr;
     s.tri_tan = (const float4 *)v->tri_tan;
     s.node = (const float4 *)v->node;
-    // the device copies: wide breadth-first nodes (rt_bvh_layout.h), triangles padded by one
-    // (a leaf lane of trav_step_w reads 4 x 16 B per triangle)
-    static thread_local std::vector<float> wide, tri;
-    wide = rtd::wide_nodes(rtd::bfs_nodes(std::vector<float>(v->node, v->node + 8 * (size_t)v->n_nodes)));
+    // the device copy of the triangles is padded (a leaf lane reads 4 x 16 B of its last
+    // triangle: its 3 records and the next one's first)
+    static thread_local std::vector<float> tri;
     tri.assign(v->tri, v->tri + 12 * (size_t)v->n_tris);
     tri.resize(tri.size() + 12, 0.f);
-    s.node_w = (const float4 *)wide.data();
     s.tri = (const float4 *)tri.data();
     s.light = (const float4 *)v->light;
     s.light_node = (const float4 *)v->light_node;
@@ -45,101 +43,20 @@ static rtd::DevScene make(const rt_scene_view *v) {
     return s;
 }
 
-// render_pixel with the stepped traversal of the wave kernel (rt_wave.h)
-template <bool COUNT>
-static rtv::V3 render_pixel_stepped(const rtd::DevScene &sc, int i, int j, int spp, rtd::Counters &cnt) {
-    rtd::Rng rng;
-    uint32_t seed = (uint32_t)(j * sc.width + i) % 2147483647u;
-    rng.x = seed == 0 ? 1u : seed;
-    rng.saved_avail = 0;
-    rng.saved = 0.f;
-    rtv::V3 sum{0.f, 0.f, 0.f};
-    for (int s = 0; s < spp; ++s) {
-        float ox = rtd::rng_offset(rng);
-        float oy = rtd::rng_offset(rng);
-        rtd::Ray r = rtd::camera_ray(sc, i, j, ox, oy);
-        sum = rtv::add(sum, rtd::trace_sample_stepped<COUNT>(sc, r, rng, cnt));
-    }
-    return sum;
-}
-
-extern "C" void kh_render(const rt_scene_view *v, int spp, int64_t p0, int64_t p1, float *out, uint64_t *cnt, int stepped) {
+// render_pixel (rt_path.h): the reference's recursion order, closest_hit by explicit stack.
+extern "C" void kh_render(const rt_scene_view *v, int spp, int64_t p0, int64_t p1, float *out, uint64_t *cnt) {
     rtd::DevScene s = make(v);
     uint64_t c[6] = {0, 0, 0, 0, 0, 0};
 #pragma omp parallel for schedule(dynamic, 16) reduction(+ : c[:6])
     for (int64_t p = p0; p < p1; ++p) {
         rtd::Counters k{0, 0, 0, 0, 0, 0, 0};
-        rtv::V3 r = stepped ? render_pixel_stepped<true>(s, (int)(p % v->width), (int)(p / v->width), spp, k)
-                            : rtd::render_pixel<true>(s, (int)(p % v->width), (int)(p / v->width), spp, k);
+        rtv::V3 r = rtd::render_pixel<true>(s, (int)(p % v->width), (int)(p / v->width), spp, k);
         out[3 * (p - p0)] = r.x;
         out[3 * (p - p0) + 1] = r.y;
         out[3 * (p - p0) + 2] = r.z;
         c[0] += k.rays; c[1] += k.aabb; c[2] += k.tri; c[3] += k.lq; c[4] += k.laabb; c[5] += k.ltri;
     }
     std::memcpy(cnt, c, sizeof c);
-}
-
-// Emulates rt_wave_kernel (raytracing-hw_amd/csrc/rt_device.hip) on the host: `waves`
-// waves of 64 lanes run round-robin one main-loop iteration at a time, sharing the pixel
-// queue; every phase uses the same rt_wave.h lane functions as the device kernel.
-extern "C" int kh_render_wave(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
-                              float *out, uint64_t *cnt_out) {
-    rtd::DevScene sc = make(v);
-    int64_t rows = 0;
-    for (int r = 0; r < v->height; ++r)
-        if ((r / row_block) % world == rank) ++rows;
-    rtd::ShardGeom g{v->width, rank, world, row_block, (long long)rows * v->width};
-    std::vector<rtd::Lane> lanes((size_t)waves * 64);
-    std::vector<char> exhausted(waves, 0), done(waves, 0);
-    for (auto &L : lanes) rtd::lane_init(L);
-    rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    unsigned queue = 0;
-    int live = waves;
-    while (live > 0) {
-        for (int w = 0; w < waves; ++w) {
-            if (done[w]) continue;
-            rtd::Lane *W = &lanes[(size_t)w * 64];
-            if (!exhausted[w]) {
-                uint64_t m = 0;
-                for (int l = 0; l < 64; ++l) if (W[l].pix < 0) m |= 1ull << l;
-                if (m) {
-                    unsigned base = queue;
-                    unsigned cm = (unsigned)__builtin_popcountll(m);
-                    queue += cm;
-                    for (int l = 0; l < 64; ++l) {
-                        if (!(m >> l & 1)) continue;
-                        long long p = (long long)base + __builtin_popcountll(m & ((1ull << l) - 1ull));
-                        if (p < g.n_pixels) rtd::lane_assign(W[l], sc, g, p);
-                    }
-                    if ((long long)base + cm >= g.n_pixels) exhausted[w] = 1;
-                }
-            }
-            bool any = false;
-            for (int l = 0; l < 64; ++l) any |= W[l].pix >= 0;
-            if (!any) { done[w] = 1; --live; continue; }
-            for (int l = 0; l < 64; ++l)
-                if (W[l].pix >= 0 && W[l].state == rtd::L_IDLE) rtd::lane_start_sample<true>(W[l], sc, g, cnt);
-            bool trav[64];
-            for (int l = 0; l < 64; ++l) trav[l] = W[l].state == rtd::L_TRAV;
-            for (;;) {
-                bool a = false;
-                for (int l = 0; l < 64; ++l) a |= trav[l];
-                if (!a) break;
-                for (int l = 0; l < 64; ++l)
-                    if (trav[l]) {
-                        if (W[l].t.sp < 0 || W[l].t.sp >= rtd::kStack) return -1;
-                        trav[l] = rtd::trav_step<true>(sc, W[l].r, W[l].t, W[l].stk, cnt);
-                    }
-            }
-            for (int l = 0; l < 64; ++l) {
-                if (W[l].state == rtd::L_TRAV) W[l].state = rtd::L_SHADE;
-                if (W[l].state == rtd::L_SHADE) rtd::lane_shade<true>(W[l], sc, spp, out, cnt);
-            }
-        }
-    }
-    uint64_t c[7] = {cnt.rays, cnt.aabb, cnt.tri, cnt.lq, cnt.laabb, cnt.ltri, cnt.hits};
-    std::memcpy(cnt_out, c, sizeof c);
-    return 0;
 }
 
 // Emulates the wavefront path (wf_init / wf_extend / wf_shade in rt_device.hip) on the host:
@@ -222,12 +139,13 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
     }
 }
 
-// Emulates rt_mega_kernel (kernel 4): `waves` waves of 64 lanes, round-robin one main-loop
+// Emulates rt_mega_kernel (kernel 0): `waves` waves of 64 lanes, round-robin one main-loop
 // iteration at a time, sharing the pixel queue, with the kernel's shade_min decision.
 // LSPLIT: the light-split kernel (light-pdf walk as lane states M_LTRAV / M_LREADY).
+// order (may be NULL): queue item p renders shard pixel order[p], as in the ordered render.
 template <bool LSPLIT>
 static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves, int shade_min,
-                       float *out, uint64_t *cnt_out) {
+                       const int32_t *order, float *out, uint64_t *cnt_out) {
     rtd::DevScene sc = make(v);
     sc.n_tris = (int)v->n_tris;
     sc.n_nodes = (int)v->n_nodes;
@@ -252,7 +170,6 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     const rtd::GlobalNodes nodes{sc.node};
     std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
     std::vector<std::vector<uint2>> stacks((size_t)waves * 64, std::vector<uint2>(rtd::kStack));
-    std::vector<std::vector<uint32_t>> stacks_c((size_t)waves * 64, std::vector<uint32_t>(rtd::kStack));
     for (auto &L : lanes) { L.pix = -1; L.state = rtd::M_IDLE; }
     std::vector<char> exhausted(waves, 0), done(waves, 0);
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -272,7 +189,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                     for (int l = 0; l < 64; ++l) {
                         if (!(m >> l & 1)) continue;
                         const long long p = base + __builtin_popcountll(m & ((1ull << l) - 1ull));
-                        if (p < n) rtd::mega_assign<true>(W[l], sc, g, p, root, cnt);
+                        if (p < n) rtd::mega_assign<true>(W[l], sc, g, order ? order[p] : (int)p, root, cnt);
                     }
                     if (base + cm >= n) exhausted[w] = 1;
                 }
@@ -287,11 +204,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
             if (!any) { done[w] = 1; --live; continue; }
             const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
             for (int l = 0; l < 64; ++l) {
-#if RT_WIDE
-                rtd::ArrayStack3 S{stacks[(size_t)w * 64 + l].data(), stacks_c[(size_t)w * 64 + l].data()};
-#else
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
-#endif
                 rtd::g_mega_slot = (long long)w * 64 + l;
                 rtd::mega_iterate<true, decltype(S), decltype(nodes), false, LSPLIT>(W[l], shade_now, sc, g, st, spp, out,
                                                                                    nullptr, root, S, nodes, cnt);
@@ -303,16 +216,12 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     return 0;
 }
 extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
-                              int shade_min, float *out, uint64_t *cnt_out) {
-    return render_mega<false>(v, spp, rank, world, row_block, waves, shade_min, out, cnt_out);
+                              int shade_min, const int32_t *order, float *out, uint64_t *cnt_out) {
+    return render_mega<false>(v, spp, rank, world, row_block, waves, shade_min, order, out, cnt_out);
 }
 extern "C" int kh_render_mega_lsplit(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
                                      int shade_min, float *out, uint64_t *cnt_out) {
-#if RT_WIDE
-    return -1;   // the light-split path is built without RT_WIDE only
-#else
-    return render_mega<true>(v, spp, rank, world, row_block, waves, shade_min, out, cnt_out);
-#endif
+    return render_mega<true>(v, spp, rank, world, row_block, waves, shade_min, nullptr, out, cnt_out);
 }
 
 // box_pair_hit (rt_wavefront.h) against box_hit_pt on each box of the pair, over `n`
@@ -363,39 +272,6 @@ extern "C" long long kh_box_pair_check(long long n, uint32_t seed) {
             ok = ok && (a == b || (want != want && got != got));   // (traversal only compares it)
         }
         bad += !ok;
-    }
-    return bad;
-}
-
-// sqrt_gt(x, a) (rt_wavefront.h: the traversal's cull without the sqrt) against
-// sqrtf(x) > a, for squared lengths x and distances a >= 0: random pairs, x at and around
-// a^2 and around the squares of a's neighbours, special values.  Returns mismatches.
-extern "C" long long kh_sqrt_gt_check(long long n, uint32_t seed) {
-    uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1;
-    auto next = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
-    auto bits = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
-    auto ubits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
-    long long bad = 0;
-    auto check = [&](float x, float a) {
-        if (rtd::sqrt_gt(x, a) != (sqrtf(x) > a)) ++bad;
-    };
-    const float specials[] = {0.f, -0.f, 1e-45f, 1e-38f, 1e9f, 3.4e38f, __builtin_inff(), __builtin_nanf("")};
-    for (float x : specials)
-        for (float a : {0.f, -0.f, 1e-45f, 1e-20f, 1.f, 1e9f, 3e38f}) check(x, a);
-    for (long long k = 0; k < n; ++k) {
-        // a: any positive finite float (uniform in bits), or a typical distance
-        const uint64_t r = next();
-        float a = (r & 1) ? bits((uint32_t)(r >> 8) % 0x7f800000u) : (float)((r >> 16) & 0xffffff) / 65536.f;
-        const double a2 = (double)a * (double)a;
-        const float x0 = (float)a2;
-        // x around a^2 (a few ulps each way) and around the midpoint square
-        const float n1 = bits(ubits(a) + 1u);
-        const float mid2 = (float)(((double)a + (double)n1) * ((double)a + (double)n1) / 4.0);
-        for (int d = -3; d <= 3; ++d) {
-            if (x0 > 0.f) check(bits(ubits(x0) + (uint32_t)d), a);
-            if (mid2 > 0.f) check(bits(ubits(mid2) + (uint32_t)d), a);
-        }
-        check(bits((uint32_t)(next() >> 8) % 0x7f800000u), a);
     }
     return bad;
 }

@@ -63,12 +63,12 @@ def _f(u):
     return np.asarray(u, np.uint32).view(np.float32)
 
 
-def ref_arrays(rt, name, width, height, spp):
-    """Flattened arrays of the reference's own parsed + BVH-built scene (golden dump),
-    completed with this build's camera constants and decoded texels (pinned equal to the
-    reference's by test_loader)."""
+def ref_arrays(rt, name, width, height, spp, dump=None):
+    """Flattened arrays of the reference's own parsed + BVH-built scene (golden dump, or
+    `dump` as loaded by rtdump), completed with this build's camera constants and decoded
+    texels (pinned equal to the reference's by test_loader)."""
     mine = rt.Scene.load(scene_path(name), width, height, spp).view()
-    d = golden(f"{name}_dump.rtd")
+    d = golden(f"{name}_dump.rtd") if dump is None else dump
     n = len(d["obj_mesh_id"])
     a = dict(mine)
     a["tri"] = np.concatenate([d["obj_position"].reshape(n, 9), d["obj_geo_normal"]], 1).astype(np.float32)

@@ -38,9 +38,9 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 2
-    assert ctypes.sizeof(rt.RtParams) == 32
-    assert ctypes.sizeof(rt.RtStats) == 9 * 8 + 3 * 8 + 3 * 8
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 3
+    assert ctypes.sizeof(rt.RtParams) == 36
+    assert ctypes.sizeof(rt.RtStats) == 9 * 8 + 3 * 8 + 3 * 8 + 3 * 8
 
 
 @pytest.mark.parametrize("height,world,rb", [(1080, 1, 8), (1080, 2, 8), (1080, 3, 8), (1080, 8, 8), (17, 3, 4),
@@ -88,8 +88,13 @@ def test_errors_are_reported(rt, tmp_path):
     assert rt.lib().rt_last_error()
     s = rt.Scene.load(rtref.scene_path("cornell"), 8, 8, 1)
     lib = rt.lib()
-    p = rt.RtParams(1, 0, 1, 8, 0, 0, 0, 0)
+    p = rt.RtParams(1, 0, 1, 8, 0, 0, 0, 0, 0)
     assert lib.rt_render(s.handle, ctypes.byref(p), None, None) == -1   # RT_ERR_ARG
+    out = np.zeros(8 * 8 * 3, np.float32)
+    assert lib.rt_render_multi(s.handle, ctypes.byref(p), 1, None, None) == -1   # RT_ERR_ARG
+    if rt.device_count() == 0:   # no GPU: every render entry fails loudly (no CPU fallback)
+        assert lib.rt_render(s.handle, ctypes.byref(p), out.ctypes.data_as(rt._c_f), None) == -4   # RT_ERR_DEVICE
+        assert lib.rt_render_multi(s.handle, ctypes.byref(p), 0, out.ctypes.data_as(rt._c_f), None) == -4
     assert lib.rt_tonemap_u8(None, 4, 4, 1, None) == -1
 
 

@@ -2,11 +2,11 @@
 reference's own per-pixel sums and counters (tests/golden, made by oracle/ref_harness).
 
 Three schedules of the same per-pixel arithmetic are checked bit-exactly:
-  * render_pixel      (rt_path.h, kernels 1 and 2: recursive-order closest_hit),
-  * stepped traversal (rt_wave.h, the wave megakernel's trav_step),
-  * wavefront         (rt_wavefront.h slot functions, the default render path:
-                       closest_hit_wf with both-children fetch and 8-byte frames),
-plus the wave-kernel emulation with several waves sharing the pixel queue.
+  * render_pixel      (rt_path.h: the reference's recursion order, closest_hit by stack),
+  * wavefront         (rt_wavefront.h slot functions, kernel 4: closest_hit_wf with the
+                       sibling-pair fetch and 8-byte frames),
+  * lane-resident     (rt_mega.h, kernel 0, the default: several waves of 64 lanes sharing
+                       the pixel queue, batched shading, any pixel order).
 """
 import ctypes
 import os
@@ -21,7 +21,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "native", "kernel_host.cpp")
 CASES = [("cornell", 33, 17, 3), ("cornell", 64, 64, 8), ("cornell_blob", 48, 48, 4),
          ("practice6_1", 256, 256, 4), ("sponza_mini", 64, 36, 4)]
-FAST = [("cornell", 33, 17, 3), ("cornell_blob", 48, 48, 4), ("sponza_mini", 64, 36, 4)]
 
 
 def _build_kh(tmp_path_factory, *defines):
@@ -30,32 +29,22 @@ def _build_kh(tmp_path_factory, *defines):
                     "-std=c++17", "-shared", "-fPIC", *defines, SRC, "-o", out], check=True)
     lib = ctypes.CDLL(out)
     V, I, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
-    lib.kh_render.argtypes = [V, I, L, L, V, V, I]
+    lib.kh_render.argtypes = [V, I, L, L, V, V]
     lib.kh_render.restype = None
-    lib.kh_render_wave.argtypes = [V, I, I, I, I, I, V, V]
-    lib.kh_render_wave.restype = I
     lib.kh_render_wf.argtypes = [V, I, I, I, I, V, V, V]
     lib.kh_render_wf.restype = I
-    lib.kh_render_mega.argtypes = [V, I, I, I, I, I, I, V, V]
+    lib.kh_render_mega.argtypes = [V, I, I, I, I, I, I, V, V, V]
     lib.kh_render_mega.restype = I
     lib.kh_render_mega_lsplit.argtypes = [V, I, I, I, I, I, I, V, V]
     lib.kh_render_mega_lsplit.restype = I
     lib.kh_box_pair_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
     lib.kh_box_pair_check.restype = ctypes.c_int64
-    lib.kh_sqrt_gt_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
-    lib.kh_sqrt_gt_check.restype = ctypes.c_int64
     return lib
 
 
 @pytest.fixture(scope="module")
 def kh(tmp_path_factory):
     return _build_kh(tmp_path_factory)
-
-
-@pytest.fixture(scope="module")
-def kh_wide(tmp_path_factory):
-    """The lane-resident kernel with the two-level traversal step (rt_trav_wide.h, RT_WIDE=1)."""
-    return _build_kh(tmp_path_factory, "-DRT_WIDE=1")
 
 
 def _golden(name, w, h, s):
@@ -68,15 +57,12 @@ def _view(rt, name, w, h, s):
 
 
 @pytest.mark.parametrize("name,w,h,s", CASES)
-@pytest.mark.parametrize("stepped", [0, 1])
-def test_pixel_schedules_match_reference(rt, kh, name, w, h, s, stepped):
-    if stepped and (name, w, h, s) not in FAST:
-        pytest.skip("stepped traversal covered on the fast cases")
+def test_pixel_schedule_matches_reference(rt, kh, name, w, h, s):
     want, cnt_want = _golden(name, w, h, s)
     v, keep = _view(rt, name, w, h, s)
     out = np.zeros((h * w, 3), np.float32)
     cnt = np.zeros(6, np.uint64)
-    kh.kh_render(ctypes.addressof(v), s, 0, w * h, out.ctypes.data, cnt.ctypes.data, stepped)
+    kh.kh_render(ctypes.addressof(v), s, 0, w * h, out.ctypes.data, cnt.ctypes.data)
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert list(cnt) == list(cnt_want)
 
@@ -107,18 +93,6 @@ def test_wavefront_shards_reassemble(rt, kh, world):
         assert kh.kh_render_wf(ctypes.addressof(v), s, rank, world, 4, out.ctypes.data, cnt.ctypes.data, None) == 0
         frame[rows] = out.reshape(len(rows), w, 3)
     assert np.array_equal(rtref.bits(frame.reshape(-1, 3)), rtref.bits(want))
-
-
-@pytest.mark.parametrize("waves", [1, 3])
-def test_wave_kernel_emulation(rt, kh, waves):
-    name, w, h, s = "cornell_blob", 48, 48, 4
-    want, cnt_want = _golden(name, w, h, s)
-    v, keep = _view(rt, name, w, h, s)
-    out = np.zeros((h * w, 3), np.float32)
-    cnt = np.zeros(7, np.uint64)
-    assert kh.kh_render_wave(ctypes.addressof(v), s, 0, 1, 8, waves, out.ctypes.data, cnt.ctypes.data) == 0
-    assert np.array_equal(rtref.bits(out), rtref.bits(want))
-    assert list(cnt[:6]) == list(cnt_want)
 
 
 def test_scene_sampler_matches_reference(rt, kh):
@@ -165,9 +139,26 @@ def test_lane_resident_emulation(rt, kh, name, w, h, s, waves, shade_min):
     v, keep = _view(rt, name, w, h, s)
     out = np.zeros((h * w, 3), np.float32)
     cnt = np.zeros(7, np.uint64)
-    assert kh.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data, cnt.ctypes.data) == 0
+    assert kh.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, None, out.ctypes.data,
+                             cnt.ctypes.data) == 0
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert list(cnt[:6]) == list(cnt_want)
+
+
+@pytest.mark.parametrize("name,w,h,s,waves", [("cornell_blob", 48, 48, 4, 2), ("sponza_mini", 64, 36, 4, 3)])
+def test_lane_resident_any_pixel_order(rt, kh, name, w, h, s, waves):
+    """The ordered render (rt_device.hip launch_order: queue item p renders pixel order[p])
+    gives the same bits for any permutation: reversed, and a seeded shuffle."""
+    want, cnt_want = _golden(name, w, h, s)
+    v, keep = _view(rt, name, w, h, s)
+    rng = np.random.default_rng(5)
+    for order in (np.arange(w * h, dtype=np.int32)[::-1].copy(), rng.permutation(w * h).astype(np.int32)):
+        out = np.zeros((h * w, 3), np.float32)
+        cnt = np.zeros(7, np.uint64)
+        assert kh.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, 48, order.ctypes.data, out.ctypes.data,
+                                 cnt.ctypes.data) == 0
+        assert np.array_equal(rtref.bits(out), rtref.bits(want))
+        assert list(cnt[:6]) == list(cnt_want)
 
 
 @pytest.mark.parametrize("name,w,h,s,waves,shade_min", [("practice6_1", 256, 256, 4, 6, 48), ("sponza_mini", 64, 36, 4, 3, 1),
@@ -186,21 +177,6 @@ def test_lane_resident_light_split_emulation(rt, kh, name, w, h, s, waves, shade
     assert list(cnt[:6]) == list(cnt_want)
 
 
-@pytest.mark.parametrize("name,w,h,s,waves,shade_min", [("cornell_blob", 48, 48, 4, 2, 32), ("sponza_mini", 64, 36, 4, 3, 1),
-                                                        ("cornell", 64, 64, 8, 2, 48)])
-def test_lane_resident_wide_traversal(rt, kh_wide, name, w, h, s, waves, shade_min):
-    """RT_WIDE=1: two node levels / two triangles per iteration from the wide breadth-first
-    node array (rt_bvh_layout.h); bit-exact sums and reference counters."""
-    want, cnt_want = _golden(name, w, h, s)
-    v, keep = _view(rt, name, w, h, s)
-    out = np.zeros((h * w, 3), np.float32)
-    cnt = np.zeros(7, np.uint64)
-    assert kh_wide.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data,
-                                  cnt.ctypes.data) == 0
-    assert np.array_equal(rtref.bits(out), rtref.bits(want))
-    assert list(cnt[:6]) == list(cnt_want)
-
-
 @pytest.mark.parametrize("leaf_n", [1, 3, 4])
 def test_lane_resident_leaf_triangles(rt, tmp_path_factory, leaf_n):
     """RT_LEAF_N (default 2, covered by the tests above): 1, 3 or 4 triangles of a leaf per
@@ -211,7 +187,7 @@ def test_lane_resident_leaf_triangles(rt, tmp_path_factory, leaf_n):
         v, keep = _view(rt, name, w, h, s)
         out = np.zeros((h * w, 3), np.float32)
         cnt = np.zeros(7, np.uint64)
-        assert kh_n.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, out.ctypes.data,
+        assert kh_n.kh_render_mega(ctypes.addressof(v), s, 0, 1, 8, waves, shade_min, None, out.ctypes.data,
                                    cnt.ctypes.data) == 0
         assert np.array_equal(rtref.bits(out), rtref.bits(want))
         assert list(cnt[:6]) == list(cnt_want)
@@ -222,10 +198,3 @@ def test_box_pair_matches_single_box_test(kh):
     primitive.cpp:146-208, restated op for op) on 4 M random cases rich in special values:
     signed zeros, infinities, NaN, flat and inverted boxes, planes through the origin."""
     assert kh.kh_box_pair_check(4_000_000, 7) == 0
-
-
-def test_sqrt_gt_matches_sqrtf(kh):
-    """sqrt_gt (trav_step_n's far-child cull on the squared entry distance) equals
-    sqrtf(x) > a on 2 M distances, with x at and around a^2 and the midpoint square, and
-    special values; the traversal's decisions therefore stay the reference's."""
-    assert kh.kh_sqrt_gt_check(2_000_000, 11) == 0

@@ -1,20 +1,20 @@
 """Host scene path: glTF loader, BVH build, light list, textures — against the reference's own
-parsed and BVH-built scene (tests/golden/*_dump.rtd, written by oracle/ref_harness `dump`).
+parsed and BVH-built scene (tests/golden/*_dump.rtd, written by oracle/ref_harness `dump`, i.e.
+the reference's sources compiled as its CMake build compiles them: GCC 11, -O3).
 
-cornell and sponza_mini are bit-exact (triangles, attributes, tangents, BVH nodes, light BVH,
-materials, normal transforms, decoded texels).  cornell_blob and practice6_1 have rotated
-meshes: the reference's scene_parser.o, built by GCC 11 at -O3, lets the SLP vectorizer drop
-float roundings in those transforms, so their vertices differ from the source
-semantics by a few ulp and the SAH build then splits differently; for them the test checks
-the triangle set within a relative 1e-5, and the render parity tests use the reference's
-own arrays through rt_scene_from_view.
+Every fixture is bit-exact (triangles, attributes, tangents, BVH nodes, light BVH, materials,
+normal transforms, decoded texels), rotated meshes included: the loader reproduces the
+roundings of the shipped binary's SLP-vectorized transform loop (rt_host.cpp
+m4_mul_vector_gcc), which differ from the source's in a few ulp.  test_slp_evidence shows the
+difference is the compiler's: the same sources built with -fno-tree-slp-vectorize give other
+arrays, which this loader does not match.
 """
 import numpy as np
 import pytest
 
 import rtref
 
-EXACT = ["cornell", "sponza_mini"]
+EXACT = ["cornell", "sponza_mini", "cornell_blob", "practice6_1"]
 ROTATED = ["cornell_blob", "practice6_1"]
 KEYS = ["tri", "tri_attr", "tri_tan", "node", "light", "light_node", "mesh_f", "mesh_tex", "mesh_normal_transform"]
 
@@ -35,7 +35,7 @@ def test_loader_bit_exact(rt, name):
     assert int(mine["ray_depth"]) == int(d["ray_depth"][0])
 
 
-@pytest.mark.parametrize("name", EXACT + ROTATED)
+@pytest.mark.parametrize("name", EXACT)
 def test_camera_matches_reference(rt, name):
     mine = _mine(rt, name)
     cam = rtref.golden(f"{name}_dump.rtd")["camera"]
@@ -45,27 +45,25 @@ def test_camera_matches_reference(rt, name):
 
 
 @pytest.mark.parametrize("name", ROTATED)
-def test_loader_rotated_within_tolerance(rt, name):
+def test_slp_evidence(rt, tmp_path, name):
+    """The reference's scene_parser.cpp built without GCC's SLP vectorizer (oracle/Makefile
+    ref_harness_noslp; needs the reference build, i.e. this container) yields different vertex
+    arrays for the rotated meshes, and this loader matches the shipped -O3 build instead."""
+    import os
+    import subprocess
+    exe = os.path.join(rtref.ROOT, "oracle", "_ref", "ref_harness_noslp")
+    if not os.path.exists(exe):
+        pytest.skip("reference build absent (oracle/_ref is built only where /root/reference exists)")
+    out = str(tmp_path / "noslp.rtd")
+    subprocess.run([exe, "dump", rtref.scene_path(name), "64", "64", out], check=True, capture_output=True)
+    noslp = rtref.ref_arrays(rt, name, 64, 64, 1, dump=rtref.rtdump.load(out))
+    slp = rtref.ref_arrays(rt, name, 64, 64, 1)
     mine = _mine(rt, name)
-    d = rtref.golden(f"{name}_dump.rtd")
-    n = len(d["obj_mesh_id"])
-    assert mine["tri"].shape[0] == n
-    ref_v0 = d["obj_position"].reshape(n, 9)[:, :3].astype(np.float64)
-    my_v0 = np.asarray(mine["tri"])[:, :3].astype(np.float64)
-    ref_id = d["obj_mesh_id"].astype(np.int64)
-    my_id = np.asarray(mine["tri_attr"])[:, 15].view(np.int32).astype(np.int64)
-
-    def order(v, ids):
-        key = np.round(v * 1e3).astype(np.int64)
-        return np.lexsort((key[:, 2], key[:, 1], key[:, 0], ids))
-
-    a, b = my_v0[order(my_v0, my_id)], ref_v0[order(ref_v0, ref_id)]
-    scale = np.maximum(np.abs(b), 1.0)
-    assert np.max(np.abs(a - b) / scale) < 1e-5
-    # materials and the light list do not depend on the transforms
-    for k in ["light", "mesh_f", "mesh_tex", "mesh_normal_transform"]:
-        ref = rtref.ref_arrays(rt, name, 64, 64, 1)
-        assert np.array_equal(np.ascontiguousarray(mine[k]).view(np.uint8), np.ascontiguousarray(ref[k]).view(np.uint8)), k
+    def raw(a):
+        return np.ascontiguousarray(a).view(np.uint8)
+    assert not np.array_equal(raw(noslp["tri"]), raw(slp["tri"]))      # the two builds disagree
+    assert np.array_equal(raw(mine["tri"]), raw(slp["tri"]))            # this loader = the shipped build
+    assert np.array_equal(raw(mine["node"]), raw(slp["node"]))
 
 
 def test_texels_match_reference(rt):
