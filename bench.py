@@ -9,17 +9,28 @@ finished to the 8-bit frame on each GPU (rt_tonemap_u8_device, scene.cpp:54-64) 
 all-gathered over RCCL (6.2 MB).  Rank 0 prints one JSON line.
 
 value    = scene closest-hit queries (rays, counted in-kernel during warmup; the count is
-           deterministic per frame) of all ranks x K / max-over-ranks wall time of the K steps
+           deterministic per frame) of all ranks x K / max-over-ranks wall time of the K steps.
+           Every frame is rendered from scratch: the heaviest-first pixel order comes from a
+           counting pre-pass inside the same call (rt_device.hip launch_order), inside the
+           timed region; nothing measured in one frame is reused by the next.
+cold_ms_per_step = the very first frame after the scene upload (one-time workspace
+           allocation and code-object load included), max over ranks.
+natural_order = the same frame in row-major pixel order (RT_FLAG_NATURAL_ORDER, no pre-pass).
 roofline = rank 0's render kernel.  Default (kernel 0, lane-resident rt_mega_kernel): one
            launch renders the frame, so achieved = the algorithmic bytes of the whole path
            (24 B per AABB test + 36 B per triangle test, scene and light BVH,
            + 156 B per shaded hit) / that launch's duration (HIP events on the launch stream).
            With --kernel 4 (wavefront) it is the extend kernel alone: 24 B per AABB test +
            36 B per triangle test + 44 B of ray/hit I/O per ray, per launch / its average
-           duration.  Peak: 8 TB/s HBM3E.
-cpu_baseline: the reference itself (oracle/_ref/ref_harness, built from /root/reference's
-           sources) timing Scene::render on the host cores over a bounded sample of the same
-           frame; falls back to the build's CPU restatement (oracle/) when _ref is absent.
+           duration.  Peak: 8 TB/s HBM3E.  `traffic` is the HBM-side bytes per launch from
+           the committed rocprofv3 PMC passes of this command (2 x FETCH_SIZE + WRITE_SIZE,
+           the guide's gfx950 correction), `traffic_undoubled` without the doubling and
+           `traffic_frac` = traffic / launch time / peak.
+cpu_baseline: the reference itself (oracle/_ref/ref_render, built from /root/reference's
+           sources) timing its Scene::render loop on every host core (nproc threads) over a
+           bounded sample of the same frame (every 8th row, 16 spp); a counting build of the
+           same sources counts its rays.  Falls back to the build's CPU restatement (oracle/)
+           when _ref is absent.
 """
 import argparse
 import json
@@ -36,6 +47,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_AABB, B_TRI, B_SHADE = 24, 36, 156
 B_RAY_IO = 24 + 4 + 16     # wf_extend per ray: ray (6 floats) + queue slot in, hit (t, u, v, prim) out
+PROFILE_PREFIX = "r01c_final"   # profiles/<prefix>_{fetch,write}_1080p256.csv of the default command
 
 
 def import_pkg():
@@ -59,8 +71,17 @@ def load_scenes_module():
     return m
 
 
-def cpu_baseline(scene_path, width, height, spp, rows, threads):
-    """Time the reference's CPU path on a bounded sample (first `rows` rows, `spp` spp).
+def cpu_quota():
+    """CPUs this process may use: the cgroup v2 quota (cpu.max), else None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def cpu_baseline(scene_path, width, height, spp, rows, stride, threads):
+    """Time the reference's CPU path on a bounded sample (`rows` rows, every `stride`-th, `spp` spp).
 
     The reference (oracle/_ref, built from /root/reference's sources by oracle/Makefile):
     ref_render runs the sample loop of Scene::render (scene.cpp:31-44) and is timed;
@@ -68,8 +89,8 @@ def cpu_baseline(scene_path, width, height, spp, rows, threads):
     ref_dir = os.path.join(ROOT, "oracle", "_ref")
     timer, counter = os.path.join(ref_dir, "ref_render"), os.path.join(ref_dir, "ref_harness")
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    sample = f"{width}x{rows} rows of the {width}x{height} frame at {spp} spp"
-    args = ["time", scene_path, str(width), str(height), str(spp), str(rows)]
+    sample = f"{rows} rows (every {stride}th) x {width} of the {width}x{height} frame at {spp} spp"
+    args = ["time", scene_path, str(width), str(height), str(spp), str(rows), str(stride)]
     if os.path.exists(timer) and os.path.exists(counter):
         try:
             def run(exe):
@@ -88,7 +109,7 @@ def cpu_baseline(scene_path, width, height, spp, rows, threads):
     import rtref
     rt = import_pkg()
     s = rt.Scene.load(scene_path, width, height, spp)
-    _, cnt, secs = rtref.Oracle().render(s.view(), spp, 0, width * rows, threads)
+    _, cnt, secs = rtref.Oracle().render(s.view(), spp, 0, width * rows, threads)   # (first rows)
     return {"value": float(cnt[0]) / secs / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": sample + " (oracle/rt_oracle.cpp restatement)", "seconds": secs}
 
@@ -106,7 +127,7 @@ def pmc_traffic(fetch_csv, write_csv, kernel_prefix):
                 return float(row[4]) * 1024.0
         return None
     f, w = mean(fetch_csv, "FETCH_SIZE"), mean(write_csv, "WRITE_SIZE")
-    return None if f is None or w is None else 2.0 * f + w
+    return None if f is None or w is None else (2.0 * f + w, f + w)
 
 
 def main():
@@ -118,11 +139,14 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--kernel", type=int, default=0, help="0 lane-resident (default), 1 one lane per pixel, "
-                    "2 persistent per pixel, 3 wave megakernel, 4 wavefront")
+    ap.add_argument("--kernel", type=int, default=0, choices=[0, 4], help="0 lane-resident (default), 4 wavefront")
     ap.add_argument("--row-block", type=int, default=8)
-    ap.add_argument("--cpu-rows", type=int, default=1080, help="rows of the frame in the CPU baseline sample")
-    ap.add_argument("--cpu-spp", type=int, default=1)
+    ap.add_argument("--cpu-rows", type=int, default=135, help="rows of the frame in the CPU baseline sample")
+    ap.add_argument("--cpu-stride", type=int, default=8, help="CPU baseline sample: every n-th row")
+    ap.add_argument("--cpu-spp", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = nproc)")
+    ap.add_argument("--natural-steps", type=int, default=1,
+                    help="timed frames in row-major pixel order (no pre-pass), reported beside the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fast-steps", type=int, default=2,
                     help="timed frames of fast mode (RT_FLAG_FAST, reported beside the headline; 0 = skip)")
@@ -168,15 +192,32 @@ def main():
     frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(count=False, fast=False):
+    def step(count=False, fast=False, natural=False):
         # render the shard, finish it to 8 bits on the GPU (scene.cpp:54-64), gather the frame
         st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
                                  count=count, kernel=args.kernel, stats=True, kernel_times=not count, fast=fast,
-                                 fast_chunk=args.fast_chunk)
+                                 fast_chunk=args.fast_chunk, device=local, natural_order=natural)
         rt.tonemap_device(out.data_ptr(), W, max_rows, S, rgb.data_ptr(), stream)
         rtdist.gather_frame(rgb, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
         return st
 
+    def timed(n, **kw):
+        """n frames between barriers + synchronize; returns (max-over-ranks seconds, stats)."""
+        sts = []
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            sts.append(step(**kw))
+        torch.cuda.synchronize()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), sts
+
+    # the very first frame of this scene on this device: nothing from an earlier render
+    cold_s, _ = timed(1)
     # warmup; the first one counts rays / tests (deterministic per frame, so valid for every step)
     counts = None
     for w in range(max(args.warmup, 1)):
@@ -185,19 +226,24 @@ def main():
             counts = st
     torch.cuda.synchronize()
 
-    kernel_ms, ext_ms, ext_n, ext_rays = [], [], [], []
+    kernel_ms, ext_ms, ext_n, ext_rays, order_ms = [], [], [], [], []
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         kernel_ms.append(st["render_ms"])
+        order_ms.append(st["order_ms"])
         ext_ms.append(st["extend_ms"])
         ext_n.append(st["extend_launches"])
         ext_rays.append(st["extend_rays"])
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+
+    natural_s = None
+    if args.natural_steps > 0 and args.kernel == 0:
+        natural_s, _ = timed(args.natural_steps, natural=True)
 
     # fast mode (RT_FLAG_FAST): same frame, per-(pixel, sample) Philox streams, samples as
     # independent work units; its own ray count (other random paths), same timing protocol
@@ -254,20 +300,20 @@ def main():
         else:
             # one launch renders the frame: the whole-path model over the launch time
             bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
-            kname = ["rt_mega_kernel", "rt_pixels_kernel", "rt_persistent_kernel", "rt_wave_kernel"][args.kernel]
+            kname = "rt_mega_kernel"
         achieved = bytes_launch / avg_s / 1e9
-        traffic, traffic_src = None, None
+        traffic, traffic_u, traffic_src = None, None, None
         if args.traffic_from != "none":
             prefix = args.traffic_from
-            default_cfg = (args.scene, W, H, S, args.kernel) == ("sponza", 1920, 1080, 256, 0)
+            default_cfg = (args.scene, W, H, S, args.kernel, world) == ("sponza", 1920, 1080, 256, 0, 1)
             if prefix == "auto":
-                prefix = os.path.join(ROOT, "profiles", "r01c_final") if default_cfg else None
+                prefix = os.path.join(ROOT, "profiles", PROFILE_PREFIX) if default_cfg else None
             if prefix:
                 fc, wc = prefix + "_fetch_1080p256.csv", prefix + "_write_1080p256.csv"
                 if os.path.exists(fc) and os.path.exists(wc):
                     t = pmc_traffic(fc, wc, "void " + kname + "<false")
                     if t is not None:
-                        traffic = t / launches
+                        traffic, traffic_u = t[0] / launches, t[1] / launches
                         traffic_src = os.path.relpath(fc, ROOT) + " + " + os.path.relpath(wc, ROOT)
         line = {
             "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",
@@ -277,6 +323,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "cold_ms_per_step": round(cold_s * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -285,24 +332,37 @@ def main():
                     "procedural RGBA8 textures; SURVEY.md App. C)",
             "config": {"workload": f"{args.scene} proxy {W}x{H}x{S}spp depth 6, one frame per step",
                        "scene": args.scene, "width": W, "height": H, "spp": S, "triangles": int(n_tris),
-                       "kernel": ["lane-resident", "pixel", "persistent-pixel", "wave", "wavefront"][args.kernel], "parallelism": f"pixel-rows x{world}",
+                       "kernel": {0: "lane-resident", 4: "wavefront"}[args.kernel],
+                       "parallelism": f"pixel-rows x{world}",
+                       "pixel_order": "heaviest-first from a counting pre-pass inside each timed frame"
+                                      if args.kernel == 0 else "row-major",
+                       "order_ms": round(float(np.mean(order_ms)), 3),
                        "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
                        "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
                        "scene_load_s": round(load_s, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else int(traffic),
+                         "traffic_undoubled": None if traffic_u is None else int(traffic_u),
+                         "traffic_frac": None if traffic is None else round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic_source": traffic_src,
                          "kernel": kname, "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
                          "launches_per_frame": launches,
                          "path_frame_bytes": int(bytes_frame), "path_frame_ms": round(frame_s * 1e3, 3),
                          "path_achieved": round(bytes_frame / frame_s / 1e9, 1)},
             "cpu_baseline": None,
+            "natural_order": None if natural_s is None else {
+                "ms_per_step": round(natural_s / args.natural_steps * 1e3, 3), "steps": args.natural_steps,
+                "value": round(rays_per_frame * args.natural_steps / natural_s / 1e6, 3), "unit": "Mrays/s",
+                "note": "RT_FLAG_NATURAL_ORDER: row-major pixel order, no pre-pass (same bits)"},
             "fast_mode": fast_line,
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(path, W, H, args.cpu_spp, min(args.cpu_rows, H), threads)
+            threads = args.cpu_threads or os.cpu_count() or 1
+            cb = cpu_baseline(path, W, H, args.cpu_spp, min(args.cpu_rows, H), args.cpu_stride, threads)
+            cb["nproc"] = os.cpu_count()
+            cb["cgroup_cpu_quota"] = cpu_quota()
+            line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

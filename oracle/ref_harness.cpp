@@ -11,7 +11,7 @@
 //
 // Modes (all print one JSON line on stdout, after the reference's own log lines):
 //   sums    <gltf> W H spp out.rtd [threads]   per-pixel float RGB sums (scene.cpp:20,42) + counters
-//   time    <gltf> W H spp [rows]              time Scene::render itself (scene.cpp:17-65)
+//   time    <gltf> W H spp [rows [stride]]     time Scene::render itself (scene.cpp:17-65)
 //   rays    <gltf> W H n out.rtd               closest-hit known answers (bvh.cpp:239-243) + per-ray test counts
 //   dump    <gltf> W H out.rtd                 post-BVH scene arrays (bvh.cpp:166 reorders objects)
 //   samplers <gltf> W H n out.rtd              SceneDistribution::sample/pdf + RNG known answers
@@ -163,12 +163,15 @@ static int mode_sums(int argc, char **argv) {
 }
 
 // Times the reference's own Scene::render (OpenMP over all pixels; shared RNG statics made
-// per-thread, otherwise unchanged).  With `rows` < H only the first `rows` rows are
-// rendered (the camera canvas keeps H so the rays are the full-frame rays).
+// per-thread, otherwise unchanged).  With `rows` < H only `rows` rows are rendered: rows 0,
+// stride, 2 * stride, ... (default stride 1: the first rows), so a bounded sample can span
+// the frame; the camera canvas keeps H, so the rays are the full-frame rays.
 static int mode_time(int argc, char **argv) {
-    if (argc < 6) throw std::runtime_error("time <gltf> W H spp [rows]");
+    if (argc < 6) throw std::runtime_error("time <gltf> W H spp [rows [stride]]");
     int W = atoi(argv[3]), H = atoi(argv[4]), spp = atoi(argv[5]);
     int rows = argc > 6 ? atoi(argv[6]) : H;
+    int stride = argc > 7 ? std::max(1, atoi(argv[7])) : 1;
+    if ((long long)(rows - 1) * stride >= H) rows = (H - 1) / stride + 1;
     Scene s = parse_scene_gltf(argv[2], W, H, spp);
     reset_counters();
     double t0 = now_s(), t1;
@@ -176,27 +179,28 @@ static int mode_time(int argc, char **argv) {
         s.render();
         t1 = now_s();
     } else {
-        // same loop shape as scene.cpp:31 (guided,16 collapse(2)) over the first `rows` rows
+        // same loop shape as scene.cpp:31 (guided,16 collapse(2)) over the sampled rows
         uniform_float_d offset(-0.5f, 0.5f);
         std::vector<vector3f> sample_canvas((size_t)W * rows, {0.f, 0.f, 0.f});
 #pragma omp parallel for schedule(guided, 16) collapse(2)
-        for (int j = 0; j < rows; ++j) {
+        for (int k = 0; k < rows; ++k) {
             for (int i = 0; i < W; ++i) {
+                const int j = k * stride;
                 Engine rng = rng::get_generator(j * W + i);
-                for (int k = 0; k < spp; ++k) {
+                for (int q = 0; q < spp; ++q) {
                     vector2f po{offset(rng), offset(rng)};
                     vector2i pp{i, j};
                     Ray r = s.camera->cast_in_pixel(pp, po);
                     r.power = s.ray_depth;
                     auto inter = s.intersect(r, rng);
-                    sample_canvas[j * W + i] += inter.color;
+                    sample_canvas[(size_t)k * W + i] += inter.color;
                 }
             }
         }
         t1 = now_s();
     }
     char extra[128];
-    std::snprintf(extra, sizeof extra, ", \"pixels\": %lld, \"spp\": %d", (long long)W * rows, spp);
+    std::snprintf(extra, sizeof extra, ", \"pixels\": %lld, \"spp\": %d, \"stride\": %d", (long long)W * rows, spp, stride);
     print_counts("time", total_counters(), t1 - t0, omp_get_max_threads(), extra);
     return 0;
 }

@@ -42,7 +42,21 @@ using rtd::shard_row;
 // Tuned constants of the default kernel (measured values in DESIGN.md §5-6).
 constexpr int kMegaWpe = 5;          // waves per SIMD the register allocation targets (96 VGPRs)
 constexpr int kShadeMin = 48;        // a wave shades once this many lanes are READY (or none traverses)
-constexpr int kOrderSpp = 2;         // samples per pixel of the counting pre-pass that orders pixels
+// Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
+// Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
+// a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
+// unfiltered (1470 ms: a noisy order loses the coherence of row-major order and gains
+// nothing), 2 spp 5 x 5 (1407 ms), 8 spp 3 x 3 (1429 ms); 8-way shards, slowest of the 8:
+// 346 ms against 478 ms in row-major order.  Ordering 64-pixel runs instead of pixels keeps
+// rows coherent but loses the spread (8-way 476 ms).
+#ifndef RT_ORDER_SPP
+#define RT_ORDER_SPP 1
+#endif
+#ifndef RT_ORDER_RADIUS
+#define RT_ORDER_RADIUS 4
+#endif
+constexpr int kOrderSpp = RT_ORDER_SPP;        // samples per pixel of the counting pre-pass
+constexpr int kOrderRadius = RT_ORDER_RADIUS;  // box filter of the pre-pass costs ((2r+1)^2 pixels)
 constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units per pixel
 constexpr int kWfRefill = 8;         // wavefront extend: idle lanes before a wave refills
 constexpr unsigned kWfChunk = 64;    // wavefront extend: queue entries claimed per atomic
@@ -271,6 +285,21 @@ __global__ void __launch_bounds__(256) rt_fast_reduce_kernel(const float *__rest
 __global__ void __launch_bounds__(256) rt_order_iota_kernel(int *ids, long long n) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) ids[i] = (int)i;
+}
+
+// Pixel order, optional smoothing: box sums of the pre-pass costs over (2r+1) shard pixels
+// along a row (dir 0) or down a column (dir 1) of the shard's rows x width grid.
+__global__ void __launch_bounds__(256) rt_order_box_kernel(const unsigned *in, unsigned *out, long long n, int width,
+                                                           int r, int dir) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const long long rows = n / width, k = p / width, i = p % width;
+    unsigned s = 0;
+    for (int d = -r; d <= r; ++d) {
+        const long long kk = dir ? k + d : k, ii = dir ? i : i + d;
+        if (kk >= 0 && kk < rows && ii >= 0 && ii < width) s += in[kk * width + ii];
+    }
+    out[p] = s;
 }
 
 // Pixel order, step 2: `sorted` holds the shard pixels heaviest first.  The first claims of
@@ -731,8 +760,9 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
 // Heaviest-first, spread pixel order for a parity-mode render of shard g, built inside the
 // frame: a counting fast-mode pre-pass of kOrderSpp samples per pixel measures each pixel's
 // traversal work (its own Philox streams: the pre-pass never touches the render's RNG), a
-// radix sort ranks the pixels by it, and rt_order_spread_kernel deals the heaviest ones out
-// over the render's `groups` waves.  Results never depend on the order; it only shortens the
+// box filter turns that into an estimate of the pixel's expected work, a radix sort ranks
+// the pixels by it, and rt_order_spread_kernel deals the heaviest ones out over the render's
+// `groups` waves.  Results never depend on the order; it only shortens the
 // frame's tail.  Returns the order in d_order.
 int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, long long groups, int **d_order) {
     const long long n = g.n_pixels;
@@ -757,6 +787,13 @@ int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, lon
                        d->counters + 8, d->queue + 1, (const int *)nullptr, cost, kOrderSpp);
     HIP_TRY(hipGetLastError());
     const unsigned nb = (unsigned)((n + 255) / 256);
+    if (kOrderRadius > 0) {   // box-filtered costs: the pixel's neighbourhood estimates its expected work
+        hipLaunchKernelGGL(rt_order_box_kernel, dim3(nb), dim3(256), 0, stream, (const unsigned *)cost, cost_sorted, n,
+                           g.width, kOrderRadius, 0);
+        hipLaunchKernelGGL(rt_order_box_kernel, dim3(nb), dim3(256), 0, stream, (const unsigned *)cost_sorted, cost, n,
+                           g.width, kOrderRadius, 1);
+        HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(rt_order_iota_kernel, dim3(nb), dim3(256), 0, stream, ids, n);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, cost, cost_sorted, ids, sorted, (int)n, 0, 32,

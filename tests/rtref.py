@@ -51,6 +51,20 @@ def scenes_module():
     return m
 
 
+def scene_sha256(directory, scene):
+    """sha256 over a generated scene's files (name + bytes, sorted by name): the value
+    tools/make_goldens.py records for the BASELINE-config goldens."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(directory) if f == scene + ".gltf" or f.startswith(scene + "_tex")
+                   or f == scene + ".bin")
+    for f in files:
+        h.update(f.encode())
+        with open(os.path.join(directory, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def golden(name):
     return rtdump.load(os.path.join(GOLD, name))
 
@@ -63,11 +77,12 @@ def _f(u):
     return np.asarray(u, np.uint32).view(np.float32)
 
 
-def ref_arrays(rt, name, width, height, spp, dump=None):
+def ref_arrays(rt, name, width, height, spp, dump=None, path=None):
     """Flattened arrays of the reference's own parsed + BVH-built scene (golden dump, or
     `dump` as loaded by rtdump), completed with this build's camera constants and decoded
-    texels (pinned equal to the reference's by test_loader)."""
-    mine = rt.Scene.load(scene_path(name), width, height, spp).view()
+    texels (pinned equal to the reference's by test_loader).  path: the scene's .gltf when it
+    is not a committed fixture."""
+    mine = rt.Scene.load(path or scene_path(name), width, height, spp).view()
     d = golden(f"{name}_dump.rtd") if dump is None else dump
     n = len(d["obj_mesh_id"])
     a = dict(mine)

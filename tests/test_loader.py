@@ -100,3 +100,23 @@ def test_loader_errors(rt, tmp_path):
     bad.write_text("{ not json")
     with pytest.raises(rt.RtError):
         rt.Scene.load(str(bad), 8, 8, 1)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("scene", ["sponza", "sponza_dragon"])
+def test_large_scenes_match_reference(rt, scene):
+    """The full-size BASELINE scenes (sponza proxy, 262 k triangles; dragon-100k + sponza,
+    362 k): the generator writes the same files the goldens were made from (sha256), and
+    this loader's arrays equal the reference's post-BVH arrays (sha256 of each array,
+    recorded by tools/make_goldens.py from the reference's own dump)."""
+    import hashlib
+    import json
+    import os
+    import tempfile
+    meta = json.load(open(os.path.join(rtref.GOLD, "golden_meta.json")))["configs"][scene]
+    d = os.path.join(tempfile.gettempdir(), "rt_scenes")
+    path = rtref.scenes_module().ensure_scene(scene, d)
+    assert rtref.scene_sha256(d, scene) == meta["scene_sha256"]
+    mine = rt.Scene.load(path, 64, 64, 1).view()
+    got = {k: hashlib.sha256(np.ascontiguousarray(mine[k]).tobytes()).hexdigest() for k in meta["ref_layout_sha256"]}
+    assert got == meta["ref_layout_sha256"]

@@ -14,6 +14,16 @@ Outputs (tests/golden/):
     <name>_rays.rtd                   closest-hit / light-pdf known answers (ref_harness rays)
     cornell_samplers.rtd              SceneDistribution sample/pdf + RNG sequences
     cornell_512x512x64_rowhash.rtd    BASELINE configs[1] full-size frame as per-row hashes
+    <scene>_pixels_<W>x<H>x<S>[_w<N>].rtd
+                                      BASELINE configs C3-C5 and the headline at full size and
+                                      full spp: seeded pixels of the frame (of each rank's
+                                      shard for C4, of rank 0's for C5), reference sums +
+                                      per-pixel test counts (ref_harness pixels)
+    golden_meta.json "configs"        sha256 of the generated scene files (pins the generator)
+                                      and of the reference's post-BVH arrays of the large
+                                      scenes in this build's layout (pins the loader)
+
+    python tools/make_goldens.py --configs   # only the BASELINE-config fixtures
 """
 import hashlib
 import importlib.util
@@ -30,6 +40,7 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import rtdump  # noqa: E402
+import rtref  # noqa: E402,F401  (tests/rtref.py: reference arrays in this build's layout)
 
 spec = importlib.util.spec_from_file_location("rt_scenes", os.path.join(ROOT, "raytracing-hw_amd", "scenes.py"))
 scenes = importlib.util.module_from_spec(spec)
@@ -79,7 +90,72 @@ def finish_golden(meta):
     meta["finish"] = harness("finish", os.path.join(GOLD, "finish_37x23x16.rtd"), ppm, 37, 23, 16)
 
 
+# BASELINE.json configs at their full size and spp: (name, scene, W, H, spp, world, pixels per shard)
+CONFIGS = [
+    ("c3", "sponza", 1024, 1024, 256, 1, 1024),
+    ("headline", "sponza", 1920, 1080, 256, 1, 1024),
+    ("c4", "sponza", 1920, 1080, 1024, 8, 128),     # every rank of the 8-way split
+    ("c5", "sponza_dragon", 3840, 2160, 4096, 8, 256),   # rank 0's shard of the 8-way split
+]
+SCENE_DIR = "/tmp/rt_scenes"
+
+
+def scene_sha256(scene):
+    """sha256 over the generated scene's files (name + bytes, sorted by name)."""
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(SCENE_DIR) if f == scene + ".gltf" or f.startswith(scene + "_tex")
+                   or f == scene + ".bin")
+    for f in files:
+        h.update(f.encode())
+        with open(os.path.join(SCENE_DIR, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def layout_sha256(arrays):
+    """sha256 per flattened array (this build's rt_scene_view layout)."""
+    keys = ["tri", "tri_attr", "tri_tan", "node", "light", "light_node", "mesh_f", "mesh_tex", "mesh_normal_transform"]
+    return {k: hashlib.sha256(np.ascontiguousarray(arrays[k]).tobytes()).hexdigest() for k in keys}
+
+
+def shard_pixels(W, H, world, rank, n, seed, row_block=8):
+    rows = np.array([r for r in range(H) if (r // row_block) % world == rank])
+    rng = np.random.default_rng(seed)
+    pick = rng.choice(len(rows) * W, n, replace=False)
+    pick.sort()
+    return (rows[pick // W] * W + pick % W).astype(np.int64)
+
+
+def config_goldens(meta):
+    import rtref
+    rt = rtref.package()
+    meta.setdefault("configs", {})
+    for scene in sorted({c[1] for c in CONFIGS}):
+        path = scenes.ensure_scene(scene, SCENE_DIR)
+        raw = os.path.join("/tmp", f"{scene}_dump_full.rtd")
+        harness("dump", path, 64, 64, raw)
+        ref = rtref.ref_arrays(rt, scene, 64, 64, 1, dump=rtdump.load(raw), path=path)
+        meta["configs"][scene] = {"scene_sha256": scene_sha256(scene), "ref_layout_sha256": layout_sha256(ref)}
+    for name, scene, W, H, S, world, n in CONFIGS:
+        path = os.path.join(SCENE_DIR, scene + ".gltf")
+        ranks = range(world) if name == "c4" else [0]
+        idx = np.concatenate([shard_pixels(W, H, world, r, n, 1000 + r) for r in ranks])
+        lst = f"/tmp/{name}_idx.i64"
+        idx.tofile(lst)
+        out = os.path.join(GOLD, f"{name}_{scene}_pixels_{W}x{H}x{S}" + (f"_w{world}" if world > 1 else "") + ".rtd")
+        meta["configs"][name] = {"scene": scene, "width": W, "height": H, "spp": S, "world": world,
+                                 "file": os.path.basename(out), "pixels": harness("pixels", path, W, H, S, lst, out)}
+        print(name, meta["configs"][name]["pixels"], flush=True)
+
+
 def main():
+    if "--configs" in sys.argv:
+        path = os.path.join(GOLD, "golden_meta.json")
+        meta = json.load(open(path))
+        config_goldens(meta)
+        with open(path, "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        return
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
     os.makedirs(GOLD, exist_ok=True)
@@ -114,6 +190,7 @@ def main():
     rtdump.save(os.path.join(GOLD, "cornell_512x512x64_rowhash.rtd"),
                 {"row_fnv1a": row_hash(s), "rows": rows.astype(np.int32), "row_sums": s[rows],
                  "counters": rtdump.load(full)["counters"]})
+    config_goldens(meta)
     with open(os.path.join(GOLD, "golden_meta.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print(json.dumps(meta, indent=1)[:2000])

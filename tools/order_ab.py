@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""A/B of pixel-order builds (RT_LIB=...): the 1-GPU frame in the default (pre-pass) order and
+in row-major order, and every shard of an N-way split (the max is the N-GPU frame time).
+
+    RT_LIB=raytracing-hw_amd/v1/librt_hw_amd.so python tools/order_ab.py [--world 8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="sponza")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--natural", type=int, default=1)
+    args = ap.parse_args()
+    rt = bench.import_pkg()
+    path = bench.load_scenes_module().ensure_scene(args.scene, os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes"))
+    W, H, S = args.width, args.height, args.spp
+    scene = rt.Scene.load(path, W, H, S)
+    scene.upload(0)
+    rtdist = __import__("importlib").import_module("raytracing_hw_amd.dist")
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {"lib": os.environ.get("RT_LIB", "default")}
+
+    def t(world, rank, steps, natural):
+        out = torch.zeros(rtdist.max_shard_rows(H, world) * W * 3, dtype=torch.float32, device="cuda")
+        ms, order = [], []
+        for _ in range(steps):
+            st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, stats=True,
+                                     natural_order=natural)
+            ms.append(st["render_ms"])
+            order.append(st["order_ms"])
+        return min(ms), min(order)
+
+    t(1, 0, 1, False)   # warm
+    res["full_ms"], res["full_order_ms"] = t(1, 0, args.steps, False)
+    if args.natural:
+        res["full_natural_ms"], _ = t(1, 0, args.steps, True)
+    sh = [t(args.world, r, 1, False)[0] for r in range(args.world)]
+    res[f"shard{args.world}_ms"] = [round(x, 1) for x in sh]
+    res[f"shard{args.world}_max_ms"] = max(sh)
+    if args.natural:
+        shn = [t(args.world, r, 1, True)[0] for r in range(args.world)]
+        res[f"shard{args.world}_natural_max_ms"] = max(shn)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
