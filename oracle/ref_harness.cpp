@@ -10,7 +10,9 @@
 //  — the per-pixel-reset convention every build component follows.
 //
 // Modes (all print one JSON line on stdout, after the reference's own log lines):
-//   sums    <gltf> W H spp out.rtd [threads]   per-pixel float RGB sums (scene.cpp:20,42) + counters
+//   sums    <gltf> W H spp out.rtd [threads [out.ppm]]
+//                                              per-pixel float RGB sums (scene.cpp:20,42) + counters
+//                                              (+ the reference's finished frame of them)
 //   time    <gltf> W H spp [rows [stride]]     time Scene::render itself (scene.cpp:17-65)
 //   rays    <gltf> W H n out.rtd               closest-hit known answers (bvh.cpp:239-243) + per-ray test counts
 //   dump    <gltf> W H out.rtd                 post-BVH scene arrays (bvh.cpp:166 reorders objects)
@@ -136,8 +138,26 @@ static void print_counts(const char *mode, const Counters &c, double secs, int t
                 threads, extra);
 }
 
+// Scene::render's frame finish (scene.cpp:54-64) of per-pixel sums into the canvas, then
+// Scene::draw_into / Canvas::write_to (canvas.h:76-89).
+static void finish_to_ppm(const std::vector<float> &sums, int W, int H, int spp, const char *path) {
+    Canvas canvas({W, H});
+    const float normalizer = 1.f / (float)spp;
+    const float gamma_ = 1.f / 2.2f;   // scene.h:36
+    for (int j = 0; j < H; ++j)
+        for (int i = 0; i < W; ++i) {
+            const size_t o = 3 * ((size_t)j * W + i);
+            vector3f color{sums[o], sums[o + 1], sums[o + 2]};
+            color *= normalizer;
+            color = aces_tonemap(color);
+            color = pow(color, gamma_);
+            canvas.set({i, j}, normal_to_ch8bit(color));
+        }
+    canvas.write_to(path);
+}
+
 static int mode_sums(int argc, char **argv) {
-    if (argc < 7) throw std::runtime_error("sums <gltf> W H spp out.rtd [threads]");
+    if (argc < 7) throw std::runtime_error("sums <gltf> W H spp out.rtd [threads [out.ppm]]");
     int W = atoi(argv[3]), H = atoi(argv[4]), spp = atoi(argv[5]);
     int threads = argc > 7 ? atoi(argv[7]) : omp_get_max_threads();
     Scene s = parse_scene_gltf(argv[2], W, H, spp);
@@ -158,6 +178,7 @@ static int mode_sums(int argc, char **argv) {
     std::vector<uint64_t> cv{c.rays, c.aabb, c.tri, c.lqueries, c.laabb, c.ltri};
     d.put("counters", cv);
     d.close();
+    if (argc > 8) finish_to_ppm(out, W, H, spp, argv[8]);   // the reference's final image of these sums
     print_counts("sums", c, t1 - t0, threads);
     return 0;
 }
@@ -520,19 +541,7 @@ static int mode_finish(int argc, char **argv) {
         }
         sums[k] = v;
     }
-    Canvas canvas({W, H});
-    const float normalizer = 1.f / (float)spp;
-    const float gamma_ = 1.f / 2.2f;   // scene.h:36
-    for (int j = 0; j < H; ++j)
-        for (int i = 0; i < W; ++i) {
-            const size_t o = 3 * ((size_t)j * W + i);
-            vector3f color{sums[o], sums[o + 1], sums[o + 2]};
-            color *= normalizer;
-            color = aces_tonemap(color);
-            color = pow(color, gamma_);
-            canvas.set({i, j}, normal_to_ch8bit(color));
-        }
-    canvas.write_to(argv[3]);
+    finish_to_ppm(sums, W, H, spp, argv[3]);
     RtDump d(argv[2]);
     d.put("sums", sums, {(uint64_t)H, (uint64_t)W, 3});
     d.put("spp", std::vector<int32_t>{spp});

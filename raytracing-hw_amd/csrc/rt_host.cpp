@@ -399,18 +399,34 @@ struct Loader {
     std::string base;
     std::vector<std::string> buffers;
 
+    // Every element of the accessor must lie inside its buffer (tightly packed: byteStride is
+    // ignored, as scene_parser.cpp does); a malformed file is RT_ERR_FORMAT, never a read
+    // past the end.
     AccessorView view(int idx) {
+        if (idx < 0) throw rt_error(RT_ERR_FORMAT, "accessor out of range");
         const rtj::Value &a = doc["accessors"][(size_t)idx];
         if (a.is_null()) throw rt_error(RT_ERR_FORMAT, "accessor out of range");
-        const rtj::Value &bv = doc["bufferViews"][(size_t)a["bufferView"].integer(0)];
+        const int bvi = a["bufferView"].integer(-1);
+        if (bvi < 0) throw rt_error(RT_ERR_FORMAT, "bufferView out of range");
+        const rtj::Value &bv = doc["bufferViews"][(size_t)bvi];
+        if (bv.is_null()) throw rt_error(RT_ERR_FORMAT, "bufferView out of range");
         int b = bv["buffer"].integer(0);
         if (b < 0 || (size_t)b >= buffers.size()) throw rt_error(RT_ERR_FORMAT, "buffer out of range");
-        size_t off = (size_t)bv["byteOffset"].number(0) + (size_t)a["byteOffset"].number(0);
+        const double off_d = bv["byteOffset"].number(0) + a["byteOffset"].number(0), count_d = a["count"].number(0);
+        if (!(off_d >= 0) || !(count_d >= 0) || off_d > 1e15 || count_d > 1e15)
+            throw rt_error(RT_ERR_FORMAT, "accessor offset / count invalid");
         AccessorView v;
-        v.count = (size_t)a["count"].number(0);
+        const size_t off = (size_t)off_d;
+        v.count = (size_t)count_d;
         v.ctype = a["componentType"].integer(0);
         v.type = a["type"].str;
-        if (off > buffers[b].size()) throw rt_error(RT_ERR_FORMAT, "accessor beyond buffer");
+        const size_t comps = v.type == "SCALAR" ? 1 : v.type == "VEC2" ? 2 : v.type == "VEC3" ? 3 : v.type == "VEC4" ? 4
+                           : v.type == "MAT4" ? 16 : 0;
+        const size_t cbytes = (v.ctype == 5120 || v.ctype == 5121) ? 1 : (v.ctype == 5122 || v.ctype == 5123) ? 2
+                            : (v.ctype == 5125 || v.ctype == 5126) ? 4 : 0;
+        const size_t size = buffers[b].size();
+        if (off > size || (comps * cbytes > 0 && v.count > (size - off) / (comps * cbytes)))
+            throw rt_error(RT_ERR_FORMAT, "accessor beyond buffer");
         v.data = (const uint8_t *)buffers[b].data() + off;
         return v;
     }
@@ -573,6 +589,7 @@ static void load_gltf(rt_scene &S, const std::string &path, int width, int heigh
             if (pv.ctype != 5126) throw rt_error(RT_ERR_FORMAT, "Position component type not supported");
             const float *pos_v = (const float *)pv.data;
             const float *nrm_v = nullptr, *tc_v = nullptr, *tan_v = nullptr;
+            size_t n_attr = pv.count;   // vertices every present attribute holds (indices must be below)
             // NB: the reference only reads the index count when NORMAL exists
             // (scene_parser.cpp:233-234); without it its count is indeterminate.  Here the
             // accessor's count is used in both cases.
@@ -583,27 +600,32 @@ static void load_gltf(rt_scene &S, const std::string &path, int width, int heigh
                 if (nv.type != "VEC3") throw rt_error(RT_ERR_FORMAT, "Normal type not supported");
                 if (nv.ctype != 5126) throw rt_error(RT_ERR_FORMAT, "Normal component type not supported");
                 nrm_v = (const float *)nv.data;
+                n_attr = std::min(n_attr, nv.count);
             }
             if (attrs.has("TEXCOORD_0")) {
                 AccessorView tv = L.view(attrs["TEXCOORD_0"].integer(0));
                 if (tv.type != "VEC2") throw rt_error(RT_ERR_FORMAT, "Texcoord type not supported");
                 if (tv.ctype != 5126) throw rt_error(RT_ERR_FORMAT, "Texcoord component type not supported");
                 tc_v = (const float *)tv.data;
+                n_attr = std::min(n_attr, tv.count);
             }
             if (attrs.has("TANGENT")) {
                 AccessorView tv = L.view(attrs["TANGENT"].integer(0));
                 if (tv.type != "VEC4") throw rt_error(RT_ERR_FORMAT, "Tangent type not supported");
                 if (tv.ctype != 5126) throw rt_error(RT_ERR_FORMAT, "Tangent component type not supported");
                 tan_v = (const float *)tv.data;
+                n_attr = std::min(n_attr, tv.count);
             }
             if (indices_ctype != 5123 && indices_ctype != 5125)
                 throw rt_error(RT_ERR_FORMAT, "Index component type not supported");
             const int mesh_id = (int)meshes.size() - 1;
             for (size_t t = 0; t < indices_count / 3; ++t) {
                 size_t index[3];
-                for (int v = 0; v < 3; ++v)
+                for (int v = 0; v < 3; ++v) {
                     index[v] = indices_ctype == 5123 ? ((const uint16_t *)iv.data)[t * 3 + v]
                                                      : ((const uint32_t *)iv.data)[t * 3 + v];
+                    if (index[v] >= n_attr) throw rt_error(RT_ERR_FORMAT, "vertex index beyond an attribute accessor");
+                }
                 Prim pr;
                 pr.mesh_id = mesh_id;
                 V3 q[3];

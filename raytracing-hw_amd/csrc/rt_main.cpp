@@ -1,8 +1,10 @@
-// rt_main.cpp — drop-in CLI for the reference's `solution` (src/main.cpp:22-60):
+// rt_main.cpp — drop-in CLI for the reference's `solution` (src/main.cpp:22-60, run.sh:2):
 //   rt_solution input.gltf width height samples [output.ppm]
 // Same positional arguments, same default output name, same terminate-with-message
-// behaviour on errors (std::runtime_error), rendering on the MI355X through librt_hw_amd.
+// behaviour on errors (std::runtime_error), rendering through librt_hw_amd on every GPU of
+// the node (rt_render_multi: one row-block shard per device; RT_GPUS=n uses devices 0..n-1).
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <iostream>
 #include <iomanip>
@@ -33,19 +35,19 @@ int main(int argc, char *argv[]) {
     std::cout << "Scene loaded: " << std::setprecision(2) << std::chrono::duration<double>(t1 - t0).count()
               << " seconds." << std::endl;
     std::cout << std::setprecision(6) << "Rendering scene." << std::endl;
-    check(rt_scene_upload(scene, 0));
+    const char *g = std::getenv("RT_GPUS");
+    const int n_gpus = g ? std::atoi(g) : 0;   // 0: every visible device
     rt_params p{};
     p.spp = samples;
-    p.world = 1;
     p.row_block = 8;
     std::vector<float> sum((size_t)width * height * 3);
     rt_stats st{};
-    check(rt_render(scene, &p, sum.data(), &st));
+    check(rt_render_multi(scene, &p, n_gpus, sum.data(), &st));
     std::vector<uint8_t> rgb((size_t)width * height * 3);
     check(rt_tonemap_u8(sum.data(), width, height, samples, rgb.data()));
     double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::cout << "      " << total << " seconds (" << total * 1000 << " ms) elapsed; render kernel "
-              << st.render_ms << " ms." << std::endl;
+    std::cout << "      " << total << " seconds (" << total * 1000 << " ms) elapsed; render " << st.render_ms
+              << " ms on " << st.devices << " MI355X." << std::endl;
     check(rt_write_ppm(output.c_str(), rgb.data(), width, height));
     std::cout << "Frame drawn into " << output << std::endl;
     rt_scene_free(scene);

@@ -120,3 +120,41 @@ def test_large_scenes_match_reference(rt, scene):
     mine = rt.Scene.load(path, 64, 64, 1).view()
     got = {k: hashlib.sha256(np.ascontiguousarray(mine[k]).tobytes()).hexdigest() for k in meta["ref_layout_sha256"]}
     assert got == meta["ref_layout_sha256"]
+
+
+def test_loader_rejects_malformed_buffers(rt, tmp_path):
+    """A truncated .bin, an accessor running past its buffer, or a vertex index beyond an
+    attribute accessor is RT_ERR_FORMAT (never a read past the end of a buffer)."""
+    import json
+    import os
+    import shutil
+    src = os.path.dirname(rtref.scene_path("cornell"))
+    doc = json.load(open(rtref.scene_path("cornell")))
+    binname = doc["buffers"][0]["uri"]
+
+    def variant(tag, mutate_doc=None, truncate=None):
+        d = tmp_path / tag
+        shutil.copytree(src, d)
+        g = json.loads(json.dumps(doc))
+        if mutate_doc:
+            mutate_doc(g)
+        (d / "cornell.gltf").write_text(json.dumps(g))
+        if truncate is not None:
+            data = (d / binname).read_bytes()
+            (d / binname).write_bytes(data[:truncate(len(data))])
+        return str(d / "cornell.gltf")
+
+    prim = doc["meshes"][0]["primitives"][0]
+    pos_acc = prim["attributes"]["POSITION"]
+
+    def shrink_positions(g):
+        g["accessors"][pos_acc]["count"] = 2
+
+    def huge_count(g):
+        g["accessors"][prim["indices"]]["count"] = 10 ** 9
+
+    for path in (variant("trunc", truncate=lambda n: n // 2), variant("count", huge_count),
+                 variant("index", shrink_positions)):
+        with pytest.raises(rt.RtError):
+            rt.Scene.load(path, 8, 8, 1)
+    rt.Scene.load(variant("ok"), 8, 8, 1)   # the unmodified copy still loads
