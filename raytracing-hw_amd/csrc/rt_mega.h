@@ -166,16 +166,17 @@ __device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc
 
 // Shade the lane's closest hit (one vertex of scene.cpp:85-154); bounce, or end the path:
 // fold, accumulate, next sample or pixel done.
-template <bool COUNT, bool FAST = false>
+template <bool COUNT, bool FAST = false, class Stack>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
-                                           int spp, float *out, unsigned *cost, const NodeRec &root, Counters &cnt) {
+                                           int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
+                                           Counters &cnt) {
     LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     const Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
     bool next = false;
     if (h.prim >= 0 && h.t < sc.max_distance) {
         Rng rng = lane_rng(L);
-        const bool cont = shade_hit<COUNT>(sc, L.r, h, rng, cnt, P, c.nv);
+        const bool cont = shade_hit<COUNT>(sc, L.r, h, rng, cnt, P, c.nv, stk);   // (stack free: T.sp == 0)
         lane_rng_set(L, rng);
         if (cont && c.power > 0) {
             c.power -= 1;
@@ -352,7 +353,7 @@ __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const 
         }
     }
     if (shade_now) {
-        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, cnt);
+        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt);
     } else if (L.state == M_TRAV) {
         if (trav_step<COUNT>(sc, L.r, L.T, stk, nodes, cnt)) L.state = M_READY;
     }

@@ -370,16 +370,17 @@ __device__ bool closest_hit(const DevScene &sc, const Ray &r, Hit &best, Counter
 
 // ManyLightsDistribution::pdf (random.cpp:179-188) over BVH::intersectAll (bvh.cpp:245-279):
 // every emissive triangle hit, left subtree before right, no root test, summed in visit order.
-template <bool COUNT>
-__device__ float light_pdf(const DevScene &sc, V3 point, V3 direction, Counters &cnt) {
+// `stk` holds the walk's node ids (.x); the lane-resident kernel passes the lane's traversal
+// stack (LDS), free while its lane shades, instead of a private array in scratch memory.
+template <bool COUNT, class Stack>
+__device__ float light_pdf(const DevScene &sc, V3 point, V3 direction, Counters &cnt, Stack &stk) {
     if (COUNT) cnt.lq++;
     Ray r = make_ray(point, direction);
-    uint32_t stk[kStack];
     int sp = 0;
-    stk[sp++] = 0;
+    stk.put(sp++, make_uint2(0u, 0u));
     float prob = 0.f;
     while (sp > 0) {
-        const uint32_t id = stk[--sp];
+        const uint32_t id = stk.get(--sp).x;
         NodeRec nd = load_node(sc.light_node, id);
         if ((nd.b & 3u) == 3u) {
             const uint32_t first = nd.a, count = nd.b >> 2;
@@ -401,11 +402,23 @@ __device__ float light_pdf(const DevScene &sc, V3 point, V3 direction, Counters 
             if (COUNT) cnt.laabb += 2;
             const bool hl = aabb_hit(l.mn, l.mx, r, e);
             const bool hr = aabb_hit(rr.mn, rr.mx, r, e);
-            if (hr) stk[sp++] = left + 1;
-            if (hl) stk[sp++] = left;
+            RT_CHECK(sp + 2 <= kStack, 13, sp, sp = 0);
+            if (hr) stk.put(sp++, make_uint2(left + 1, 0u));
+            if (hl) stk.put(sp++, make_uint2(left, 0u));
         }
     }
     return prob / (float)sc.n_lights;
+}
+// A private stack (host tests, the ray-level entry, the wavefront shade kernel).
+struct LocalStack {
+    uint32_t id[kStack];
+    __device__ __forceinline__ void put(int i, uint2 v) { id[i] = v.x; }
+    __device__ __forceinline__ uint2 get(int i) const { return make_uint2(id[i], 0u); }
+};
+template <bool COUNT>
+__device__ float light_pdf(const DevScene &sc, V3 point, V3 direction, Counters &cnt) {
+    LocalStack stk;
+    return light_pdf<COUNT>(sc, point, direction, cnt, stk);
 }
 
 // ------------------------------------------------------------------------ textures
@@ -606,10 +619,16 @@ __device__ __forceinline__ V3 scene_sample(const DevScene &sc, V3 pos, V3 N, V3 
 }
 
 // SceneDistribution::pdf (random.cpp:210-218)
+template <bool COUNT, class Stack>
+__device__ __forceinline__ float scene_pdf(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, V3 dir, Counters &cnt,
+                                           Stack &stk) {
+    if (!sc.n_lights) return (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
+    return (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt, stk) + vndf_pdf(N, eye, r2, dir)) / 3;
+}
 template <bool COUNT>
 __device__ __forceinline__ float scene_pdf(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, V3 dir, Counters &cnt) {
-    if (!sc.n_lights) return (cosine_pdf(N, dir) + vndf_pdf(N, eye, r2, dir)) / 2;
-    return (cosine_pdf(N, dir) + light_pdf<COUNT>(sc, pos, dir, cnt) + vndf_pdf(N, eye, r2, dir)) / 3;
+    LocalStack stk;
+    return scene_pdf<COUNT>(sc, pos, N, eye, r2, dir, cnt, stk);
 }
 
 // The records of one path slot in HBM for the wavefront pipeline, vertex-major so a vertex
@@ -833,14 +852,21 @@ __device__ __forceinline__ bool shade_post(const DevScene &sc, const V3 rd, cons
 // and, if the path continues, its BRDF factors), advances nv and replaces r by the bounce
 // ray.  Returns false where the recursion returns at this vertex (sample below the surface,
 // pdf <= 0 or NaN).
-template <bool COUNT, class Rec>
-__device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
+// `stk`: the light walk's stack (see light_pdf).
+template <bool COUNT, class Rec, class Stack>
+__device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv,
+                          Stack &stk) {
     ShadeMid m;
     if (!shade_pre<COUNT>(sc, r, hit, rng, cnt, P, nv, m)) return false;
     RT_PROF_BEGIN
-    const float pdf = scene_pdf<COUNT>(sc, m.pos, m.N, rtv::neg(r.d), m.r2, m.dir, cnt);
+    const float pdf = scene_pdf<COUNT>(sc, m.pos, m.N, rtv::neg(r.d), m.r2, m.dir, cnt, stk);
     RT_PROF_SEG(4);
     return shade_post(sc, r.d, m, pdf, P, nv, r);
+}
+template <bool COUNT, class Rec>
+__device__ bool shade_hit(const DevScene &sc, Ray &r, const Hit &hit, Rng &rng, Counters &cnt, Rec &P, int &nv) {
+    LocalStack stk;
+    return shade_hit<COUNT>(sc, r, hit, rng, cnt, P, nv, stk);
 }
 
 // Backward fold over the recorded vertices (a primary miss gives bg colour 0).

@@ -466,9 +466,14 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
 #ifdef __HIPCC__
 // Device stack: the first K entries in LDS (entry k of thread t at [k * 256 + t], so a
 // wave's 64 lanes hit consecutive 8-byte words), deeper entries in scratch.  K = 8 holds
-// 96% of all pushes on the sponza frame (tools: RT_STACK_PROBE histogram).
+// 96% of all pushes on the sponza frame (tools: RT_STACK_PROBE histogram), yet the scratch
+// frames of the other 4% were the largest share of the kernel's HBM writes (scratch lines
+// leave L2 before they are read back).  K = 11 fills the lane-resident kernel's block to
+// 30 KB of LDS (5 blocks per CU still fit): sponza 1080p x256spp 1401 -> 1364 ms, WRITE_SIZE
+// 124 -> 101 B per ray at K = 10; K = 12 (32 KB) drops a block per CU (1544 ms)
+// (profiles/r02_lds_stack_ab.jsonl).
 #ifndef RT_LDS_STACK
-#define RT_LDS_STACK 8
+#define RT_LDS_STACK 11
 #endif
 constexpr int kLdsStack = RT_LDS_STACK;   // stack frames per lane in LDS (deeper ones spill to scratch)
 __shared__ uint2 wf_lds_stack[kLdsStack * 256];   // blocks of 256 threads
