@@ -845,6 +845,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (rc) return rc;
         } else {   // lane-resident (rt_mega.h), the default
             if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "ray_depth must be in [1, 15]");
+            if (spp >= (1 << 20)) return rt_fail(RT_ERR_LIMIT, "rt_render: spp must be < 2^20");
             // fast mode (RT_FLAG_FAST): work units of `cs` samples, Philox seed per sample, at
             // most kFastMaxChunks units per pixel (partials: pixels x chunks x 12 B)
             int cs = 0, chunks = 1;

@@ -36,7 +36,8 @@ enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREAD
 
 struct MegaLane {
     int pix;         // shard pixel (slot), -1 = none (the host keeps shards below 2^31 pixels)
-    int s, power, nv, state;
+    uint32_t ctr;    // LaneCtr packed: sample (bits 0-19), depth budget (20-23), vertices (24-28)
+    int state;
     // fast mode only (RT_FLAG_FAST): work unit = samples [s, send) of the pixel; its partial
     // sum goes to dst; gpix = j*W+i keys the per-sample Philox seed.  Unused fields of the
     // parity kernel are dropped by the compiler.
@@ -89,16 +90,17 @@ __device__ __forceinline__ Rng lane_rng(const MegaLane &L) { return L.rng; }
 __device__ __forceinline__ void lane_rng_set(MegaLane &L, const Rng &r) { L.rng = r; }
 #endif
 
-// The lane's sample counter, depth budget and recorded-vertex count (registers; measured
-// no faster in LDS).
+// The lane's sample counter, depth budget and recorded-vertex count, packed in one register
+// (samples < 2^20, ray_depth <= 15, vertices <= 16: checked by the host) so the loop state
+// that stays live through the shading code is two registers smaller.
 struct LaneCtr {
     int s, power, nv;
 };
-__device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &L) { return LaneCtr{L.s, L.power, L.nv}; }
+__device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &L) {
+    return LaneCtr{(int)(L.ctr & 0xfffffu), (int)((L.ctr >> 20) & 15u), (int)(L.ctr >> 24)};
+}
 __device__ __forceinline__ void lane_ctr_set(MegaLane &L, const LaneCtr &c) {
-    L.s = c.s;
-    L.power = c.power;
-    L.nv = c.nv;
+    L.ctr = (uint32_t)c.s | (uint32_t)c.power << 20 | (uint32_t)c.nv << 24;
 }
 
 // Closest-hit query start for L.r: BVH::intersect's counters and root box (bvh.cpp:239-243).
