@@ -113,10 +113,17 @@ typedef struct {
  * walk as its own traversal state between two shading passes.  Same bits; measured slower
  * on every scene tried, so off by default. */
 #define RT_FLAG_LIGHT_SPLIT 4
-/* Parity mode renders pixels heaviest-first: a counting pre-pass of 2 samples per pixel
- * (its own Philox streams), a radix sort and a spread over the waves, all inside the call
- * and inside render_ms.  This flag renders in row-major order instead (same bits). */
+/* Parity mode renders pixels heaviest-first: a counting pre-pass of 1 sample per pixel
+ * (its own Philox streams), a box filter, a radix sort and a spread over the waves, all
+ * inside the call and inside render_ms.  This flag renders in row-major order instead (same
+ * bits). */
 #define RT_FLAG_NATURAL_ORDER 8
+/* Parity mode, once the pixel queue is empty, runs the next samples of a wave's unfinished
+ * pixels on its idle lanes before their start state is known, and adds only those whose
+ * start state is proven equal to the sequential chain's (rt_mega.h, speculative sample
+ * runahead): same bits, shorter frame tail.  This flag turns it off.  (Counting renders,
+ * count = 1, never use it: their counters are those of the sequential chain.) */
+#define RT_FLAG_NO_RUNAHEAD 16
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */

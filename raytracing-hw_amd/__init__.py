@@ -51,6 +51,7 @@ FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES
 FLAG_FAST = 2            # RT_FLAG_FAST: per-(pixel, sample) Philox-seeded streams, not bit-identical to the reference
 FLAG_LIGHT_SPLIT = 4     # RT_FLAG_LIGHT_SPLIT: light-pdf walk as its own traversal state (same bits)
 FLAG_NATURAL_ORDER = 8   # RT_FLAG_NATURAL_ORDER: row-major pixel order instead of the in-frame heaviest-first order
+FLAG_NO_RUNAHEAD = 16    # RT_FLAG_NO_RUNAHEAD: no speculative sample runahead in the waves' tails (same bits)
 
 
 class RtParams(ctypes.Structure):
@@ -212,22 +213,24 @@ class Scene:
         _check(lib().rt_scene_upload(self._h, device))
 
     def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False, fast=False, fast_chunk=0,
-                device=0, light_split=False, natural_order=False):
+                device=0, light_split=False, natural_order=False, runahead=True):
         flags = ((FLAG_KERNEL_TIMES if kernel_times else 0) | (FLAG_FAST if fast else 0) |
-                 (FLAG_LIGHT_SPLIT if light_split else 0) | (FLAG_NATURAL_ORDER if natural_order else 0))
+                 (FLAG_LIGHT_SPLIT if light_split else 0) | (FLAG_NATURAL_ORDER if natural_order else 0) |
+                 (0 if runahead else FLAG_NO_RUNAHEAD))
         return RtParams(spp or 0, rank, world, row_block, int(count), kernel, flags, fast_chunk, device)
 
     def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0, fast=False,
-                    fast_chunk=0, light_split=False, natural_order=False):
+                    fast_chunk=0, light_split=False, natural_order=False, runahead=True):
         """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42).
         fast=True: fast mode (RT_FLAG_FAST, work units of fast_chunk samples): statistically
-        equivalent to the reference, not bit-identical.  light_split / natural_order: other
-        schedules of the same bits (RT_FLAG_LIGHT_SPLIT, RT_FLAG_NATURAL_ORDER)."""
+        equivalent to the reference, not bit-identical.  light_split / natural_order /
+        runahead=False: other schedules of the same bits (RT_FLAG_LIGHT_SPLIT,
+        RT_FLAG_NATURAL_ORDER, RT_FLAG_NO_RUNAHEAD)."""
         rows = shard_rows(self.height, rank, world, row_block)
         out = np.zeros((len(rows), self.width, 3), np.float32)
         st = RtStats()
         p = self._params(spp, rank, world, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk, device=device,
-                         light_split=light_split, natural_order=natural_order)
+                         light_split=light_split, natural_order=natural_order, runahead=runahead)
         _check(lib().rt_render(self._h, ctypes.byref(p), out.ctypes.data_as(_c_f), ctypes.byref(st)))
         return out, st.as_dict()
 
@@ -242,12 +245,12 @@ class Scene:
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
                       kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0, device=0,
-                      light_split=False, natural_order=False):
+                      light_split=False, natural_order=False, runahead=True):
         """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream, on
         `device` (upload(device) first).  kernel_times: per-launch HIP-event timing of the
         wavefront kernels (needs stats).  fast: fast mode (RT_FLAG_FAST), see render_sums."""
         p = self._params(spp, rank, world, row_block, count, kernel, kernel_times, fast, fast_chunk, device,
-                         light_split, natural_order)
+                         light_split, natural_order, runahead)
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))

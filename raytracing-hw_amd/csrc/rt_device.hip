@@ -58,6 +58,10 @@ constexpr int kShadeMin = 48;        // a wave shades once this many lanes are R
 constexpr int kOrderSpp = RT_ORDER_SPP;        // samples per pixel of the counting pre-pass
 constexpr int kOrderRadius = RT_ORDER_RADIUS;  // box filter of the pre-pass costs ((2r+1)^2 pixels)
 constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units per pixel
+#ifndef RT_SPEC_PIXELS_PER_LANE
+#define RT_SPEC_PIXELS_PER_LANE 1
+#endif
+constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
 constexpr int kWfRefill = 8;         // wavefront extend: idle lanes before a wave refills
 constexpr unsigned kWfChunk = 64;    // wavefront extend: queue entries claimed per atomic
 constexpr double kWfCompactBelow = 0.75;   // wavefront: dense queue until this active fraction
@@ -188,10 +192,14 @@ __device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT
 // p renders shard pixel order[p].  `cost` (COUNT only): per-pixel traversal tests out.
 // Exit: the queue is monotonic, so once a claim reaches n_items a wave stops claiming; the
 // loop ends when no lane of the wave holds work, so the grid always drains.
-template <bool COUNT, bool FAST = false, bool LSPLIT = false>
+// SPEC (parity renders without counting): a wave whose claim finds the queue empty enters its
+// tail and runs speculative sample runahead (rt_mega.h spec_manage) on its idle lanes.  A
+// separate instantiation, so the kernel without it keeps its own register allocation.
+template <bool COUNT, bool FAST = false, bool LSPLIT = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMegaWpe, 8)))
 rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
                unsigned long long *queue, const int *order, unsigned *cost, int cs) {
+    constexpr bool kSpec = SPEC && !COUNT && !FAST && !LSPLIT;
     const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels;
     const int lane = threadIdx.x & 63;
     // texel-decode LUT in LDS: the shading's lane-dependent lookups become ds_reads
@@ -209,6 +217,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     L.pix = -1;
     L.state = rtd::M_IDLE;
     bool exhausted = false;
+    bool tail = false, wave_room = false;
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -235,7 +244,39 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 if ((long long)base + cm >= n_items) exhausted = true;
             }
         }
-        if (!__any(L.pix >= 0)) break;
+        if constexpr (kSpec) {
+            if (exhausted && !tail) {
+                if (lane == 0) rtd::spec_hint_take();
+                rtd::spec_convert(L, rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, lane);
+                tail = true;
+                wave_room = false;
+#ifdef RT_MEGA_PROF
+                if (lane == 0) RT_SPEC_STAT(7, 1);
+#endif
+            }
+            if (tail) {
+                wave_room |= rtd::spec_hint_take();
+                if (__any(L.state == rtd::M_DONE_NEW) || (wave_room && __any(L.state == rtd::M_IDLE))) {
+#ifdef RT_MEGA_PROF
+                    const long long c0 = clock64();
+#endif
+                    wave_room = rtd::spec_manage(rtd::SpecLanes{L}, sc, g,
+                                                 rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, spp,
+                                                 out, root);
+#ifdef RT_MEGA_PROF
+                    if (lane == 0) {
+                        RT_SPEC_STAT(0, 1);
+                        RT_SPEC_STAT(1, clock64() - c0);
+                    }
+#endif
+                }
+                if (!__any(L.state != rtd::M_IDLE)) break;
+            } else if (!__any(L.pix >= 0)) {
+                break;
+            }
+        } else if (!__any(L.pix >= 0)) {
+            break;
+        }
         const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
         const bool shade_now = nr > 0 && (nr >= kShadeMin || nt == 0);
@@ -249,7 +290,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         }
 #endif
         rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
-                                                                           root, S, nodes, cnt);
+                                                                           root, S, nodes, cnt, kSpec && tail);
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
@@ -303,20 +344,20 @@ __global__ void __launch_bounds__(256) rt_order_box_kernel(const unsigned *in, u
 }
 
 // Pixel order, step 2: `sorted` holds the shard pixels heaviest first.  The first claims of
-// the render (each of the `groups` waves takes 64 consecutive queue items at its start, one
-// pixel per lane, all lanes at once) get the heaviest m = min(n, groups * 64) pixels, spread
-// so that every wave holds one pixel of every cost stratum: queue item gi * 64 + j gets rank
-// r = j * a + min(j, b) + gi (m = a * 64 + b: the ranks in (lane j, wave gi) order of the
+// the render (each of the `groups` waves takes `per` consecutive queue items at its start, one
+// pixel per lane, all lanes at once) get the heaviest m = min(n, groups * per) pixels, spread
+// so that every wave holds one pixel of every cost stratum: queue item gi * per + j gets rank
+// r = j * a + min(j, b) + gi (m = a * per + b: the ranks in (lane j, wave gi) order of the
 // items that exist).  A heavy pixel's wave-mates are then light and finish early, and its
 // sequential sample chain runs in a sparse wave.  Later claims stay heaviest-first.
 __global__ void __launch_bounds__(256) rt_order_spread_kernel(const int *sorted, int *order, long long n,
-                                                              long long groups) {
+                                                              long long groups, long long per) {
     const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
-    const long long m = n < groups * 64 ? n : groups * 64;
+    const long long m = n < groups * per ? n : groups * per;
     long long r = q;
     if (q < m) {
-        const long long gi = q / 64, j = q % 64, a = m / 64, b = m % 64;
+        const long long gi = q / per, j = q % per, a = m / per, b = m % per;
         r = j * a + (j < b ? j : b) + gi;
     }
     order[q] = sorted[r];
@@ -663,12 +704,17 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     return RT_OK;
 }
 
+// 256-thread blocks of `kernel` the device holds at once.
 template <class K>
-unsigned persistent_blocks(rt_device_scene *d, K kernel, long long work) {
+long long resident_blocks(rt_device_scene *d, K kernel) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    return (long long)d->cu_count * per_cu;
+}
+template <class K>
+unsigned persistent_blocks(rt_device_scene *d, K kernel, long long work) {
     const long long need = (work + 255) / 256;
-    const long long b = std::min<long long>(need, (long long)d->cu_count * per_cu);
+    const long long b = std::min<long long>(need, resident_blocks(d, kernel));
     return (unsigned)std::max<long long>(b, 1);
 }
 
@@ -764,7 +810,8 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
 // the pixels by it, and rt_order_spread_kernel deals the heaviest ones out over the render's
 // `groups` waves.  Results never depend on the order; it only shortens the
 // frame's tail.  Returns the order in d_order.
-int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, long long groups, int **d_order) {
+int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, long long groups, long long per,
+                 int **d_order) {
     const long long n = g.n_pixels;
     // order buffer: cost, cost sorted, ids, ids sorted, order (n each), then the sort's scratch
     size_t tmp_bytes = 0;
@@ -798,7 +845,8 @@ int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, lon
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, cost, cost_sorted, ids, sorted, (int)n, 0, 32,
                                                          stream));
-    hipLaunchKernelGGL(rt_order_spread_kernel, dim3(nb), dim3(256), 0, stream, (const int *)sorted, order, n, groups);
+    hipLaunchKernelGGL(rt_order_spread_kernel, dim3(nb), dim3(256), 0, stream, (const int *)sorted, order, n, groups,
+                       per);
     HIP_TRY(hipGetLastError());
     *d_order = order;
     return RT_OK;
@@ -855,9 +903,16 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
             const long long n_items = g.n_pixels * chunks;
             const bool lsplit = !fast && (p->flags & RT_FLAG_LIGHT_SPLIT) != 0;
+            // Speculative sample runahead (rt_mega.h) where the frame is mostly tail: a shard of
+            // at most kSpecPixelsPerLane pixels per resident lane (the 8-way split of the
+            // headline: 342 -> 304 ms; at 4-way, 2 pixels per lane, it measured no gain).
+            const long long full_blocks = resident_blocks(d, rt_mega_kernel<false, false, false, true>);
+            const bool spec = !fast && !lsplit && !count && !(p->flags & RT_FLAG_NO_RUNAHEAD) &&
+                              g.n_pixels <= kSpecPixelsPerLane * full_blocks * 256;
             auto mk = fast ? (count ? rt_mega_kernel<true, true> : rt_mega_kernel<false, true>)
                            : lsplit ? (count ? rt_mega_kernel<true, false, true> : rt_mega_kernel<false, false, true>)
-                                    : (count ? rt_mega_kernel<true> : rt_mega_kernel<false>);
+                                    : count ? rt_mega_kernel<true>
+                                            : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
             const unsigned blocks = persistent_blocks(d, mk, n_items);
             int rc = ensure_wf(d, std::max<long long>(g.n_pixels, (long long)blocks * 256), s->ray_depth);   // vertex records
             if (rc) return rc;
@@ -866,7 +921,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity)
             int *order = nullptr;
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER)) {
-                rc = launch_order(d, g, stream, 4LL * blocks, &order);
+                rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
                 if (rc) return rc;
                 ordered = true;
             }
@@ -881,6 +936,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(rtd::g_spec_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
@@ -912,6 +968,13 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                              "normal=%.0f mr=%.0f sample=%.0f pdf=%.0f base+brdf=%.0f\n",
                              (double)sg[0] / pf[3], (double)sg[1] / pf[3], (double)sg[2] / pf[3],
                              (double)sg[3] / pf[3], (double)sg[4] / pf[3], (double)sg[5] / pf[3]);
+                unsigned long long sp[8];
+                HIP_TRY(hipMemcpyFromSymbolAsync(sp, HIP_SYMBOL(rtd::g_spec_prof), sizeof sp, 0, hipMemcpyDeviceToHost, stream));
+                HIP_TRY(hipStreamSynchronize(stream));
+                std::fprintf(stderr, "[mega prof] runahead: tail waves=%llu passes/tail wave=%.1f cycles/pass=%.0f "
+                             "cycles in passes/wave=%.3g frontier jobs=%llu runahead jobs=%llu added=%llu "
+                             "invalidations=%llu\n", sp[7], sp[7] ? (double)sp[0] / sp[7] : 0.0,
+                             sp[0] ? (double)sp[1] / sp[0] : 0.0, (double)sp[1] / pf[7], sp[2], sp[3], sp[4], sp[6]);
             }
 #endif
         }

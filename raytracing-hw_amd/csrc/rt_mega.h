@@ -31,8 +31,10 @@ inline long long mega_slot() { return g_mega_slot; }
 using MegaTrav = TravState;
 __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return sc.node; }
 
-// M_LTRAV / M_LREADY: light-pdf walk as its own traversal (light-split kernel, below)
-enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4 };
+// M_LTRAV / M_LREADY: light-pdf walk as its own traversal (light-split kernel, below).
+// M_DONE_NEW / M_DONE: a runahead job whose sample has ended, holding its colour and end
+// state until its pixel's frontier reaches it (speculative runahead, below).
+enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4, M_DONE_NEW = 5, M_DONE = 6 };
 
 struct MegaLane {
     int pix;         // shard pixel (slot), -1 = none (the host keeps shards below 2^31 pixels)
@@ -168,10 +170,38 @@ __device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc
 
 // Shade the lane's closest hit (one vertex of scene.cpp:85-154); bounce, or end the path:
 // fold, accumulate, next sample or pixel done.
+// Set when a lane of the wave added its sample itself (spec_job_end): its pixel may take
+// runahead jobs again, so the wave runs a management pass when a lane is idle.
+#if defined(__HIPCC__)
+__shared__ int spec_hint_lds[4];
+__device__ __forceinline__ void spec_hint_set() { spec_hint_lds[threadIdx.x >> 6] = 1; }
+__device__ __forceinline__ bool spec_hint_take() {
+    const bool h = spec_hint_lds[threadIdx.x >> 6] != 0;
+    spec_hint_lds[threadIdx.x >> 6] = 0;
+    return h;
+}
+#else
+inline thread_local bool g_spec_hint[4096];   // host harness: per emulated wave (mega_slot() / 64)
+inline void spec_hint_set() { g_spec_hint[(mega_slot() >> 6) & 4095] = true; }
+inline bool spec_hint_take() {
+    bool &h = g_spec_hint[(mega_slot() >> 6) & 4095];
+    const bool v = h;
+    h = false;
+    return v;
+}
+#endif
+
+// End of a runahead job's sample (speculative runahead, below): adds it and starts the next
+// sample on this lane when no other job of its pixel is in flight, else waits (M_DONE_NEW).
+__device__ void spec_job_end(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st, int spp,
+                             float *out, const NodeRec &root, V3 color, LaneCtr c);
+
+// `tail` (wave-uniform): the wave runs runahead jobs (spec_manage below); a job's path end
+// goes to spec_job_end instead of the pixel sum in the lane.
 template <bool COUNT, bool FAST = false, class Stack>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
-                                           Counters &cnt) {
+                                           Counters &cnt, bool tail = false) {
     LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     const Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
@@ -189,6 +219,10 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
     if (next) {
         lane_ctr_set(L, c);
         mega_begin<COUNT>(L, root, cnt);
+        return;
+    }
+    if (!COUNT && !FAST && tail) {   // runahead job: colour of sample c.s, end state in the RNG slot
+        spec_job_end(L, sc, g, st, spp, out, root, fold_path(P, c.nv), c);
         return;
     }
     const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv));
@@ -342,7 +376,8 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
 template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT = false>
 __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
-                                             const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt) {
+                                             const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt,
+                                             bool tail = false) {
     if constexpr (LSPLIT) {
         if (shade_now) {
             if (L.state == M_READY || L.state == M_LREADY)
@@ -355,10 +390,447 @@ __device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const 
         }
     }
     if (shade_now) {
-        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt);
+        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt, tail);
     } else if (L.state == M_TRAV) {
         if (trav_step<COUNT>(sc, L.r, L.T, stk, nodes, cnt)) L.state = M_READY;
     }
+}
+
+// ---------------------------------------------------------------- speculative sample runahead
+// A pixel's samples form one sequential chain (scene.cpp:34-42): sample t+1 starts from the
+// RNG state sample t ends in, and how many draws sample t takes depends on its path.  Once
+// the pixel queue is empty, a wave's lanes run out of pixels while the heavy pixels' chains
+// go on: the frame then lasts as long as its slowest chain.  Runahead lets the
+// idle lanes of the wave run the next samples of those chains before their start state is
+// known, and keeps only results whose start state is proven:
+//   * A path with v vertices calls SceneDistribution::sample v times, and the draws of one
+//     call are decided by the drawn values alone (rt_path.h rng_skip_sample).  So the state
+//     sample t ends in is rng_skip_sample(X_t, v_t), and v_t is mostly ray_depth for the
+//     pixels whose chains are long (69% of the samples of the heaviest sponza pixels).
+//   * Each pixel has a record.  Its frontier f is the first sample not yet added; X_f, the
+//     true state sample f starts from, is known once sample f-1 is added.  Jobs f, f+1, ...,
+//     nxt-1 are in flight, each on its own lane: job f from X_f, job u+1 from
+//     rng_skip_sample(start of job u, ray_depth).  An ended job waits (M_DONE) until it is the
+//     frontier.
+//   * When the frontier job has ended it is added to the pixel sum (in sample order, so the
+//     float sum is the reference's), and its end state E becomes X_{f+1}.  The jobs past it
+//     stay only if job f+1 started from E (states compared bit for bit); otherwise the
+//     record's epoch ends and the lanes running them are freed.  A result is only ever used
+//     when its start state equals the true one, so the pixel sum is bit-identical to the
+//     sequential chain's.
+// Records live in WfState::mid (the light-split kernel's planes, unused here), indexed by
+// the wave's lane that held the pixel when the wave entered its tail: plane 0 (pix, f, nxt,
+// epoch), 1 (sum xyz, meta), 2 (X_f, lane table low word), 3 (start state of job nxt-1, lane
+// table high word); plane 4 is each lane's job (tag = record | epoch << 6, start state).  A management pass loads them once, works on registers with the wave's
+// shuffles and ballots, and stores them back: one memory round trip per pass.  The same
+// pass runs on the host test harness (tests/native/kernel_host.cpp) over emulated lanes:
+// WArr is one register per lane on the GPU and a 64-entry array on the host.
+
+// Diagnostics build (RT_MEGA_PROF): runahead event counts, printed by the launch.
+// [0] management passes [1] their cycles (per wave) [2] frontier jobs issued [3] runahead jobs
+// issued [4] jobs added [5] of them runahead jobs [6] invalidations [7] waves that reached a tail
+#if defined(RT_MEGA_PROF) && defined(__HIPCC__)
+__device__ unsigned long long g_spec_prof[8];
+#define RT_SPEC_STAT(k, v) atomicAdd(&::rtd::g_spec_prof[k], (unsigned long long)(v))
+#elif !defined(__HIPCC__)
+inline unsigned long long g_spec_prof[8];   // host test harness
+#define RT_SPEC_STAT(k, v) (::rtd::g_spec_prof[k] += (unsigned long long)(v))
+#else
+#define RT_SPEC_STAT(k, v) do { } while (0)
+#endif
+
+// Record meta (plane 1 .w): bit 0 active, bit 1 X_f known (false until the wave's first job of
+// the pixel ends).  Window and issue rate measured on the 4- and 8-way shards of the headline
+// frame (profiles/r02_runahead_ab.jsonl): window 3 307 ms, 4 306, 6 316 (8-way); one runahead
+// job per pixel per pass 304.  Windows that adapt to a pixel's prediction hit rate (grow on a
+// hit, halve on a miss) measured 384: the pixels with long chains lost their runahead too.
+#ifndef RT_SPEC_WINDOW
+#define RT_SPEC_WINDOW 4
+#endif
+#ifndef RT_SPEC_ISSUE
+#define RT_SPEC_ISSUE 1
+#endif
+constexpr uint32_t kRecActive = 1u;
+constexpr uint32_t kRecXf = 2u;
+constexpr int kSpecWindow = RT_SPEC_WINDOW;   // jobs in flight per pixel at most, frontier included (<= 10)
+constexpr int kSpecIssue = RT_SPEC_ISSUE;     // runahead jobs a pixel gets per management pass
+static_assert(kSpecWindow >= 1 && kSpecWindow <= 10, "lane table holds 10 slots");
+// The lanes running jobs f, f+1, ...: 6-bit slots of a 64-bit table (planes 2 and 3 .w).
+__device__ __forceinline__ int spec_tab(unsigned long long t, int q) { return (int)((t >> (6 * q)) & 63ull); }
+__device__ __forceinline__ unsigned long long spec_tab_set(unsigned long long t, int q, int ln) {
+    return (t & ~(63ull << (6 * q))) | ((unsigned long long)ln << (6 * q));
+}
+
+struct SpecView {
+    uint4 *base;        // WfState::mid
+    long long lanes;    // plane stride (lane slots)
+    long long wbase;    // lane slot of this wave's lane 0
+    __device__ __forceinline__ uint4 *w(int plane, int r) const { return base + ((long long)plane * lanes + wbase + r); }
+};
+__device__ __forceinline__ Rng rng_unpack(uint4 v) { return Rng{v.x, v.y, __uint_as_float(v.z)}; }
+__device__ __forceinline__ bool rng_same(const Rng &a, const Rng &b) {
+    return a.x == b.x && a.saved_avail == b.saved_avail && __float_as_uint(a.saved) == __float_as_uint(b.saved);
+}
+__device__ __forceinline__ uint4 v3_pack(V3 v, uint32_t w) {
+    return make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), w);
+}
+__device__ __forceinline__ bool job_state(int s) { return s != M_IDLE; }
+
+// Per-lane values of a wave: this lane's register on the GPU (at(src) = the wave shuffle,
+// called by every lane), a 64-entry array on the host.  WAVE_PHASE runs its body for this
+// lane (GPU) or for every lane in turn (host); a phase only reads other lanes' values that an
+// earlier phase wrote.
+#if defined(__HIPCC__)
+__device__ __forceinline__ uint32_t wshfl(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+template <class T> struct WArr;
+template <> struct WArr<uint32_t> {
+    uint32_t v;
+    __device__ __forceinline__ uint32_t get(int) const { return v; }
+    __device__ __forceinline__ void put(int, uint32_t x) { v = x; }
+    __device__ __forceinline__ uint32_t at(int s) const { return wshfl(v, s); }
+};
+template <> struct WArr<int> {
+    int v;
+    __device__ __forceinline__ int get(int) const { return v; }
+    __device__ __forceinline__ void put(int, int x) { v = x; }
+    __device__ __forceinline__ int at(int s) const { return __shfl(v, s, 64); }
+};
+template <> struct WArr<Rng> {
+    Rng v;
+    __device__ __forceinline__ Rng get(int) const { return v; }
+    __device__ __forceinline__ void put(int, Rng x) { v = x; }
+    __device__ __forceinline__ Rng at(int s) const {
+        return Rng{wshfl(v.x, s), wshfl(v.saved_avail, s), __uint_as_float(wshfl(__float_as_uint(v.saved), s))};
+    }
+};
+template <> struct WArr<V3> {
+    V3 v;
+    __device__ __forceinline__ V3 get(int) const { return v; }
+    __device__ __forceinline__ void put(int, V3 x) { v = x; }
+    __device__ __forceinline__ V3 at(int s) const { return V3{__shfl(v.x, s, 64), __shfl(v.y, s, 64), __shfl(v.z, s, 64)}; }
+};
+// acc = the wave's ballot of p (acc starts at 0)
+#define WBALLOT(acc, lane, p) ((acc) = __ballot(p))
+#define WAVE_PHASE(lane, ...)                   \
+    {                                            \
+        const int lane = (int)(threadIdx.x & 63); \
+        __VA_ARGS__                              \
+    }
+struct SpecLanes {   // the wave's lanes as seen by one lane: its own MegaLane
+    MegaLane &L;
+    __device__ __forceinline__ MegaLane &operator[](int) const { return L; }
+};
+#else
+template <class T> struct WArr {
+    T v[64];
+    T get(int l) const { return v[l]; }
+    void put(int l, T x) { v[l] = x; }
+    T at(int s) const { return v[s]; }
+};
+#define WBALLOT(acc, lane, p) ((acc) |= (p) ? (1ull << (lane)) : 0ull)
+#define WAVE_PHASE(lane, ...) \
+    for (int lane = 0; lane < 64; ++lane) { __VA_ARGS__ }
+struct SpecLanes {
+    MegaLane *W;
+    MegaLane &operator[](int l) const { return W[l]; }
+};
+#endif
+
+// Position of the i-th (from 0) set bit of m (m has more than i set bits).
+__device__ __forceinline__ int nth_bit(unsigned long long m, int i) {
+    int pos = 0;
+    for (int w = 32; w > 0; w >>= 1)
+        if (__builtin_popcountll(m & ((1ull << (pos + w)) - 1ull)) <= i) pos += w;
+    return pos;
+}
+__device__ __forceinline__ int popc64(unsigned long long m) { return __builtin_popcountll(m); }
+
+// The wave enters its tail (queue empty): every lane's pixel gets a record at this lane; its
+// sample in flight is the frontier job (table slot 0 = this lane), started from the true
+// state (X_f not yet known).
+__device__ __forceinline__ void spec_convert(MegaLane &L, const SpecView &V, int lane) {
+    if (L.pix >= 0) {
+        const LaneCtr c = lane_ctr(L);
+        *V.w(0, lane) = make_uint4((uint32_t)L.pix, (uint32_t)c.s, (uint32_t)c.s + 1u, 0u);
+        *V.w(1, lane) = v3_pack(lane_sum(L), kRecActive);
+        *V.w(2, lane) = make_uint4(0u, 0u, 0u, (uint32_t)lane);   // table slot 0: this lane
+        *V.w(3, lane) = make_uint4(0u, 0u, 0u, 0u);
+        *V.w(4, lane) = make_uint4((uint32_t)lane, 0u, 0u, 0u);
+    } else {
+        *V.w(1, lane) = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// Start job (record r, sample t, epoch e) on this lane from state Y.
+__device__ __forceinline__ void spec_start(MegaLane &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
+                                           uint32_t pix, uint32_t t, const Rng &Y) {
+    L.pix = (int)pix;
+    lane_ctr_set(L, LaneCtr{(int)t, 0, 0});
+    lane_rng_set(L, Y);
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    mega_sample<false>(L, sc, g, root, cnt);
+}
+
+// A job's sample has ended (path end in a tail wave).  When it is its pixel's frontier and no
+// other job of the pixel is in flight, this lane adds it at once and goes on with the next
+// sample from its end state, as outside the tail (one record round trip instead of a wait
+// for a management pass); the record then shows job f + 1 on this lane.  Otherwise the job
+// waits for the next pass with its colour in the lane's sum slot.  Only this lane holds a job
+// of the pixel in the first case, and passes never overlap a shading step, so the record
+// update is this lane's alone.
+__device__ __forceinline__ void spec_job_end(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
+                                             int spp, float *out, const NodeRec &root, V3 color, LaneCtr c) {
+    const int lane = (int)(mega_slot() & 63);
+    const SpecView V{(uint4 *)st.mid, st.lanes, mega_slot() - lane};
+    const uint4 j = *V.w(4, lane);
+    const int r = (int)(j.x & 63u);
+    const uint4 a = *V.w(0, r), b = *V.w(1, r);
+    const uint32_t t = (uint32_t)c.s;
+    if ((j.x >> 6) == a.w && t == a.y && a.z == t + 1u && (b.w & kRecActive)) {
+        const V3 sum = rtv::add(V3{__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)}, color);
+        const Rng E = lane_rng(L);
+        const uint32_t m = b.w | kRecXf;
+        RT_SPEC_STAT(4, 1);
+        if (t + 1u == (uint32_t)spp) {
+            const long long o = 3 * (long long)a.x;
+            out[o + 0] = sum.x;
+            out[o + 1] = sum.y;
+            out[o + 2] = sum.z;
+            *V.w(0, r) = make_uint4(a.x, t + 1u, t + 1u, a.w);
+            *V.w(1, r) = v3_pack(sum, 0u);
+            L.pix = -1;
+            L.state = M_IDLE;
+            return;
+        }
+        *V.w(0, r) = make_uint4(a.x, t + 1u, t + 2u, a.w);
+        *V.w(1, r) = v3_pack(sum, m);
+        *V.w(2, r) = make_uint4(E.x, E.saved_avail, __float_as_uint(E.saved), (uint32_t)lane);   // X_f; slot 0: here
+        *V.w(3, r) = make_uint4(E.x, E.saved_avail, __float_as_uint(E.saved), 0u);   // job nxt-1 starts from E
+        *V.w(4, lane) = make_uint4(j.x, E.x, E.saved_avail, __float_as_uint(E.saved));
+        c.s = (int)t + 1;
+        lane_ctr_set(L, c);
+        Counters cnt{0, 0, 0, 0, 0, 0, 0};
+        mega_sample<false>(L, sc, g, root, cnt);
+        if (kSpecWindow > 1 && t + 2u < (uint32_t)spp) spec_hint_set();
+        return;
+    }
+    lane_sum_set(L, color);
+    lane_ctr_set(L, c);
+    L.state = M_DONE_NEW;
+}
+
+// One management pass of a tail wave: add ended frontier jobs in order, free the lanes of
+// added, superseded or invalidated jobs, hand idle lanes new jobs (first a frontier job to
+// every pixel without one, then runahead jobs in record order: at the tail's start, lane
+// order is heaviest first, rt_order_spread_kernel).  Returns whether a record can still take
+// a job (the wave calls again when a lane is idle).
+__device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc, const ShardGeom &g,
+                                            const SpecView &V, int spp, float *out, const NodeRec &root) {
+    const int depth = sc.ray_depth;
+    // records (this lane as record holder)
+    WArr<uint32_t> rp, rf, rn, re, rm, tl, th;   // tl, th: lane table
+    WArr<V3> rs;
+    WArr<Rng> rx, ry;
+    // jobs (this lane as job runner)
+    WArr<uint32_t> jt, jsamp;
+    WArr<int> js;
+    WArr<V3> jc;
+    WArr<Rng> je, jy;
+    WAVE_PHASE(lane, {
+        MegaLane &L = lanes[lane];
+        const uint4 a = *V.w(0, lane), b = *V.w(1, lane), c = *V.w(2, lane), d = *V.w(3, lane), j = *V.w(4, lane);
+        rp.put(lane, a.x);
+        rf.put(lane, a.y);
+        rn.put(lane, a.z);
+        re.put(lane, a.w);
+        rs.put(lane, V3{__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)});
+        rm.put(lane, b.w);
+        rx.put(lane, rng_unpack(c));
+        ry.put(lane, rng_unpack(d));
+        tl.put(lane, c.w);
+        th.put(lane, d.w);
+        jt.put(lane, j.x);
+        jy.put(lane, Rng{j.y, j.z, __uint_as_float(j.w)});   // plane 4: (tag, start state)
+        js.put(lane, L.state);
+        jsamp.put(lane, (uint32_t)lane_ctr(L).s);
+        const bool done = L.state == M_DONE_NEW || L.state == M_DONE;
+        jc.put(lane, done ? lane_sum(L) : V3{0.f, 0.f, 0.f});
+        je.put(lane, done ? lane_rng(L) : Rng{0u, 0u, 0.f});
+    })
+    // A. add ended frontier jobs, one per pixel per round, at most kSpecWindow rounds
+    for (int q = 0; q < kSpecWindow; ++q) {
+        WArr<int> prog;
+        WAVE_PHASE(lane, {
+            const uint32_t m = rm.get(lane);
+            const unsigned long long tab = (unsigned long long)th.get(lane) << 32 | tl.get(lane);
+            const bool has = (m & kRecActive) && rn.get(lane) > rf.get(lane);
+            const int j0 = has ? spec_tab(tab, 0) : lane;
+            const int j1 = has && rn.get(lane) > rf.get(lane) + 1u ? spec_tab(tab, 1) : lane;
+            // the frontier job's lane and the next job's lane (shuffles: every lane)
+            const int s0 = js.at(j0);
+            const uint32_t t0 = jt.at(j0), n0 = jsamp.at(j0);
+            const V3 c0 = jc.at(j0);
+            const Rng e0 = je.at(j0), y1 = jy.at(j1);
+            int pr = 0;
+            if (has && (s0 == M_DONE_NEW || s0 == M_DONE) && t0 == ((uint32_t)lane | re.get(lane) << 6) &&
+                n0 == rf.get(lane)) {
+                uint32_t f = rf.get(lane) + 1u, n = rn.get(lane), mm = m | kRecXf;
+                unsigned long long tb = tab >> 6;   // table slots 1.. -> 0..
+                const V3 sum = rtv::add(rs.get(lane), c0);
+                const bool keep = (m & kRecXf) && n > f && rng_same(y1, e0);
+                RT_SPEC_STAT(4, 1);
+                if (!keep && n > f) {   // the runahead past f started from another state
+                    re.put(lane, re.get(lane) + 1u);
+                    n = f;
+                    tb = 0ull;
+                    RT_SPEC_STAT(6, 1);
+                }
+                if (f == (uint32_t)spp) {
+                    const long long o = 3 * (long long)rp.get(lane);
+                    out[o + 0] = sum.x;
+                    out[o + 1] = sum.y;
+                    out[o + 2] = sum.z;
+                    mm = 0u;
+                }
+                rf.put(lane, f);
+                rn.put(lane, n);
+                rm.put(lane, mm);
+                tl.put(lane, (uint32_t)tb);
+                th.put(lane, (uint32_t)(tb >> 32));
+                rs.put(lane, sum);
+                rx.put(lane, e0);
+                pr = 1;
+            }
+            prog.put(lane, pr);
+        })
+        unsigned long long any = 0;
+        WAVE_PHASE(lane, { WBALLOT(any, lane, prog.get(lane) != 0); })
+        if (!any) break;
+    }
+    // job lanes: added, superseded or invalidated jobs end; ended runahead jobs wait
+    WAVE_PHASE(lane, {
+        MegaLane &L = lanes[lane];
+        const bool job = job_state(js.get(lane));
+        const int r = job ? (int)(jt.get(lane) & 63u) : lane;
+        const uint32_t fr = rf.at(r), er = re.at(r);
+        if (job) {
+            if ((jt.get(lane) >> 6) != er || jsamp.get(lane) < fr) {
+                L.state = M_IDLE;
+                L.pix = -1;
+            } else if (L.state == M_DONE_NEW) {
+                L.state = M_DONE;
+            }
+        }
+    })
+    // C1. pixels without a frontier job in flight get one, from the true state X_f
+    unsigned long long nm = 0, idle = 0;
+    WAVE_PHASE(lane, {
+        const bool need = (rm.get(lane) & kRecActive) && rn.get(lane) == rf.get(lane);
+        WBALLOT(nm, lane, need);
+        WBALLOT(idle, lane, lanes[lane].state == M_IDLE);
+    })
+    const int n_need = popc64(nm), n_idle = popc64(idle);
+    WAVE_PHASE(lane, {
+        MegaLane &L = lanes[lane];
+        const int i = popc64(idle & ((1ull << lane) - 1ull));
+        const bool issue = ((idle >> lane) & 1ull) && i < n_need;
+        const int r = issue ? nth_bit(nm, i) : lane;
+        const uint32_t pix = rp.at(r), f = rf.at(r), e = re.at(r);
+        const Rng X = rx.at(r);
+        if (issue) {
+            spec_start(L, sc, g, root, pix, f, X);
+            jt.put(lane, (uint32_t)r | e << 6);
+            jy.put(lane, X);
+            RT_SPEC_STAT(2, 1);
+        }
+        // record side: the k-th needing record got the k-th idle lane
+        const int k = popc64(nm & ((1ull << lane) - 1ull));
+        if (((nm >> lane) & 1ull) && k < n_idle) {
+            rn.put(lane, rf.get(lane) + 1u);
+            ry.put(lane, rx.get(lane));
+            tl.put(lane, (uint32_t)nth_bit(idle, k));   // slot 0 (no other jobs are in flight)
+            th.put(lane, 0u);
+        }
+    })
+    // C2. runahead: idle lanes take the next jobs of pixels with room in their window
+    WArr<int> room, incl;
+    unsigned long long idle2 = 0;
+    WAVE_PHASE(lane, {
+        int rr = 0;
+        const uint32_t m = rm.get(lane);
+        if ((m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane)) {
+            const int win = kSpecWindow - (int)(rn.get(lane) - rf.get(lane)), left = spp - (int)rn.get(lane);
+            rr = win < left ? win : left;
+            rr = rr < 0 ? 0 : (rr < kSpecIssue ? rr : kSpecIssue);
+        }
+        room.put(lane, rr);
+        WBALLOT(idle2, lane, lanes[lane].state == M_IDLE);
+    })
+#if defined(__HIPCC__)
+    {
+        int x = room.v;
+        const int lane = (int)(threadIdx.x & 63);
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, (unsigned)d, 64);
+            if (lane >= d) x += y;
+        }
+        incl.v = x;
+    }
+#else
+    for (int l = 0, t = 0; l < 64; ++l) incl.put(l, t += room.get(l));
+#endif
+    const int total = incl.at(63), n_idle2 = popc64(idle2);
+    WAVE_PHASE(lane, {
+        MegaLane &L = lanes[lane];
+        const int i = ((idle2 >> lane) & 1ull) ? popc64(idle2 & ((1ull << lane) - 1ull)) : (1 << 30);
+        int r = 0;   // first record with incl > i
+        for (int w = 32; w > 0; w >>= 1)
+            if (incl.at(r + w - 1) <= i) r += w;
+        const int incl_r = incl.at(r), room_r = room.at(r);
+        const uint32_t pix = rp.at(r), n = rn.at(r), e = re.at(r);
+        Rng Y = ry.at(r);
+        if (i < total) {
+            const int j = i - (incl_r - room_r);
+            for (int q = 0; q <= j; ++q) rng_skip_sample(Y, depth, sc.n_lights);
+            spec_start(L, sc, g, root, pix, n + (uint32_t)j, Y);
+            jt.put(lane, (uint32_t)r | e << 6);
+            jy.put(lane, Y);
+            RT_SPEC_STAT(3, 1);
+        }
+    })
+    WAVE_PHASE(lane, {   // record side: its takers are idle lanes excl .. excl + taken - 1
+        const int rr = room.get(lane), excl = incl.get(lane) - rr;
+        int taken = n_idle2 - excl < rr ? n_idle2 - excl : rr;
+        taken = taken < 0 ? 0 : taken;
+        const int last = taken > 0 ? nth_bit(idle2, excl + taken - 1) : lane;
+        const Rng yl = jy.at(last);
+        if (taken > 0) {
+            unsigned long long tb = (unsigned long long)th.get(lane) << 32 | tl.get(lane);
+            const int base = (int)(rn.get(lane) - rf.get(lane));
+            for (int q = 0; q < taken; ++q) tb = spec_tab_set(tb, base + q, nth_bit(idle2, excl + q));
+            tl.put(lane, (uint32_t)tb);
+            th.put(lane, (uint32_t)(tb >> 32));
+            rn.put(lane, rn.get(lane) + (uint32_t)taken);
+            ry.put(lane, yl);
+        }
+    })
+    // store the records and the jobs; can a record still take a job?
+    unsigned long long roomy = 0;
+    WAVE_PHASE(lane, {
+        *V.w(0, lane) = make_uint4(rp.get(lane), rf.get(lane), rn.get(lane), re.get(lane));
+        *V.w(1, lane) = v3_pack(rs.get(lane), rm.get(lane));
+        const Rng x = rx.get(lane), yy = ry.get(lane);
+        *V.w(2, lane) = make_uint4(x.x, x.saved_avail, __float_as_uint(x.saved), tl.get(lane));
+        *V.w(3, lane) = make_uint4(yy.x, yy.saved_avail, __float_as_uint(yy.saved), th.get(lane));
+        const Rng y = jy.get(lane);
+        *V.w(4, lane) = make_uint4(jt.get(lane), y.x, y.saved_avail, __float_as_uint(y.saved));
+        const uint32_t m = rm.get(lane);
+        const uint32_t f = rf.get(lane), n = rn.get(lane);
+        const bool rm_room = (m & kRecActive) &&
+                             (n == f || ((m & kRecXf) && (int)(n - f) < kSpecWindow && (int)n < spp));
+        WBALLOT(roomy, lane, rm_room);
+    })
+    return roomy != 0;
 }
 
 }  // namespace rtd

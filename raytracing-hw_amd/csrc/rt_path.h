@@ -487,6 +487,15 @@ __device__ __forceinline__ V3 cosine_sample(V3 n, Rng &r) {
 }
 __device__ __forceinline__ float cosine_pdf(V3 n, V3 d) { return rtv::smax(0.f, rtv::dot(d, n)) * kInvPiF; }
 
+// The uniform sample on a disc of visible_normal::sample (random.cpp:114-122): pairs of
+// uniform(-1, 1) draws until one lies inside the unit circle.
+__device__ __forceinline__ void disc_draw(Rng &r, float &ux, float &uy) {
+    do {
+        ux = rng_uniform_m11(r);
+        uy = rng_uniform_m11(r);
+    } while (ux * ux + uy * uy > 1.f);
+}
+
 // visible_normal::sample (random.cpp:103-134)
 __device__ __forceinline__ V3 vndf_sample(V3 n, V3 eye, float alpha, Rng &r) {
     const V3 Z{0.f, 0.f, 1.f};
@@ -497,10 +506,7 @@ __device__ __forceinline__ V3 vndf_sample(V3 n, V3 eye, float alpha, Rng &r) {
     V3 T1 = lensq > 0 ? rtv::mul(V3{-Vh.y, Vh.x, 0}, 1.f / sqrtf(lensq)) : V3{1, 0, 0};
     V3 T2 = rtv::cross(Vh, T1);
     float ux, uy;
-    do {
-        ux = rng_uniform_m11(r);
-        uy = rng_uniform_m11(r);
-    } while (ux * ux + uy * uy > 1.f);
+    disc_draw(r, ux, uy);
     float s = 0.5f + 0.5f * Vh.z;
     float ty = (1.f - s) * sqrtf(1.f - ux * ux) + s * uy;
     V3 Nh = rtv::add(rtv::add(rtv::mul(T1, ux), rtv::mul(T2, ty)),
@@ -610,12 +616,46 @@ struct SoARec {
 
 // SceneDistribution::sample (random.cpp:194-208): mixture of cosine, VNDF and light
 // sampling chosen by one uniform(-1, 1) draw.
-__device__ __forceinline__ V3 scene_sample(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, Rng &rng) {
+// The mixture draw (random.cpp:196-203): 0 cosine, 1 VNDF, 2 light.
+__device__ __forceinline__ int mixture_pick(Rng &rng, int n_lights) {
     float s = (rng_uniform_m11(rng) + 1.f) * 3 * 0.5f;
-    if (!sc.n_lights) s /= 1.5f;
-    if (s <= 1.f) return cosine_sample(N, rng);
-    if (s <= 2.f) return vndf_sample(N, eye, r2, rng);
+    if (!n_lights) s /= 1.5f;
+    return s <= 1.f ? 0 : (s <= 2.f ? 1 : 2);
+}
+__device__ __forceinline__ V3 scene_sample(const DevScene &sc, V3 pos, V3 N, V3 eye, float r2, Rng &rng) {
+    const int b = mixture_pick(rng, sc.n_lights);
+    if (b == 0) return cosine_sample(N, rng);
+    if (b == 1) return vndf_sample(N, eye, r2, rng);
     return light_sample(sc, pos, rng);
+}
+
+// The RNG draws of one sample (scene.cpp:36-41) whose path calls SceneDistribution::sample
+// k times, without the geometry: the two pixel offsets, then per call the mixture draw and
+// the chosen sampler's draws (cosine: three polar normals through the cache; VNDF: the disc
+// pairs; light: triangle choice + u + v).  Every draw count here is decided by the drawn
+// values alone; the one geometric exception (cosine_weighted::sample retries when the
+// sphere sample cancels the normal to |d| < 1e-12, random.cpp:50-53) is not modelled, so a
+// caller must compare states, not assume them (rt_mega.h spec_manage does).  Used by the
+// speculative sample runahead: a pixel's sample t+1 starts from the state sample t ends in,
+// and for a path of ray_depth vertices that state is rng_skip_sample(start of t, ray_depth).
+__device__ __forceinline__ void rng_skip_sample(Rng &r, int k, int n_lights) {
+    (void)rng_next(r);   // rng_offset x 2: one engine draw each
+    (void)rng_next(r);
+    for (int v = 0; v < k; ++v) {
+        const int b = mixture_pick(r, n_lights);
+        if (b == 0) {
+            (void)rng_normal(r);
+            (void)rng_normal(r);
+            (void)rng_normal(r);
+        } else if (b == 1) {
+            float ux, uy;
+            disc_draw(r, ux, uy);
+        } else {
+            (void)rng_next(r);
+            (void)rng_next(r);
+            (void)rng_next(r);
+        }
+    }
 }
 
 // SceneDistribution::pdf (random.cpp:210-218)

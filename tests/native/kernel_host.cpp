@@ -143,7 +143,21 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
 // iteration at a time, sharing the pixel queue, with the kernel's shade_min decision.
 // LSPLIT: the light-split kernel (light-pdf walk as lane states M_LTRAV / M_LREADY).
 // order (may be NULL): queue item p renders shard pixel order[p], as in the ordered render.
-template <bool LSPLIT>
+// SPEC: the speculative sample runahead of the waves' tails (rt_mega.h spec_*), driven here
+// by host loops over the wave's lanes where the kernel uses ballots (rt_mega.h spec_manage);
+// a non-counting render, as on the GPU.
+static uint64_t g_spec_passes = 0;   // management passes since the last kh_spec_stats
+extern "C" void kh_spec_stats(uint64_t *out) {   // passes, frontier jobs, runahead jobs, added, invalidations
+    out[0] = g_spec_passes;
+    out[1] = rtd::g_spec_prof[2];
+    out[2] = rtd::g_spec_prof[3];
+    out[3] = rtd::g_spec_prof[4];
+    out[4] = rtd::g_spec_prof[6];
+    g_spec_passes = 0;
+    std::memset(rtd::g_spec_prof, 0, sizeof rtd::g_spec_prof);
+}
+
+template <bool LSPLIT, bool SPEC = false>
 static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves, int shade_min,
                        const int32_t *order, float *out, uint64_t *cnt_out) {
     rtd::DevScene sc = make(v);
@@ -171,7 +185,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
     std::vector<std::vector<uint2>> stacks((size_t)waves * 64, std::vector<uint2>(rtd::kStack));
     for (auto &L : lanes) { L.pix = -1; L.state = rtd::M_IDLE; }
-    std::vector<char> exhausted(waves, 0), done(waves, 0);
+    std::vector<char> exhausted(waves, 0), done(waves, 0), tail(waves, 0), wave_room(waves, 0);
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
     long long queue = 0;
     int live = waves;
@@ -189,15 +203,38 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                     for (int l = 0; l < 64; ++l) {
                         if (!(m >> l & 1)) continue;
                         const long long p = base + __builtin_popcountll(m & ((1ull << l) - 1ull));
-                        if (p < n) rtd::mega_assign<true>(W[l], sc, g, order ? order[p] : (int)p, root, cnt);
+                        if (p < n) rtd::mega_assign<!SPEC>(W[l], sc, g, order ? order[p] : (int)p, root, cnt);
                     }
                     if (base + cm >= n) exhausted[w] = 1;
+                }
+            }
+            if (SPEC && exhausted[w] && !tail[w]) {
+                const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
+                for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], V, l);
+                rtd::g_mega_slot = (long long)w * 64;
+                rtd::spec_hint_take();
+                tail[w] = 1;
+                wave_room[w] = 0;
+            }
+            if (tail[w]) {
+                rtd::g_mega_slot = (long long)w * 64;
+                wave_room[w] |= rtd::spec_hint_take();
+                bool fresh = false, idle = false;
+                for (int l = 0; l < 64; ++l) {
+                    fresh |= W[l].state == rtd::M_DONE_NEW;
+                    idle |= W[l].state == rtd::M_IDLE;
+                }
+                if (fresh || (wave_room[w] && idle)) {
+                    ++g_spec_passes;
+                    wave_room[w] = rtd::spec_manage(rtd::SpecLanes{W}, sc, g,
+                                                    rtd::SpecView{(uint4 *)st.mid, st.lanes, (long long)w * 64}, spp,
+                                                    out, root);
                 }
             }
             bool any = false;
             int nr = 0, nt = 0;
             for (int l = 0; l < 64; ++l) {
-                any |= W[l].pix >= 0;
+                any |= tail[w] ? W[l].state != rtd::M_IDLE : W[l].pix >= 0;
                 nr += W[l].state == rtd::M_READY || W[l].state == rtd::M_LREADY;
                 nt += W[l].state == rtd::M_TRAV || W[l].state == rtd::M_LTRAV;
             }
@@ -206,8 +243,9 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
             for (int l = 0; l < 64; ++l) {
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
                 rtd::g_mega_slot = (long long)w * 64 + l;
-                rtd::mega_iterate<true, decltype(S), decltype(nodes), false, LSPLIT>(W[l], shade_now, sc, g, st, spp, out,
-                                                                                   nullptr, root, S, nodes, cnt);
+                rtd::mega_iterate<!SPEC, decltype(S), decltype(nodes), false, LSPLIT>(W[l], shade_now, sc, g, st, spp,
+                                                                                    out, nullptr, root, S, nodes, cnt,
+                                                                                    (bool)tail[w]);
             }
         }
     }
@@ -219,9 +257,55 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
                               int shade_min, const int32_t *order, float *out, uint64_t *cnt_out) {
     return render_mega<false>(v, spp, rank, world, row_block, waves, shade_min, order, out, cnt_out);
 }
+extern "C" int kh_render_mega_spec(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
+                                   int shade_min, const int32_t *order, float *out, uint64_t *cnt_out) {
+    return render_mega<false, true>(v, spp, rank, world, row_block, waves, shade_min, order, out, cnt_out);
+}
 extern "C" int kh_render_mega_lsplit(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
                                      int shade_min, float *out, uint64_t *cnt_out) {
     return render_mega<true>(v, spp, rank, world, row_block, waves, shade_min, nullptr, out, cnt_out);
+}
+
+// rng_skip_sample (rt_path.h, the speculative runahead's state prediction) against the
+// real sample chain: for every sample of the listed pixels (parity RNG convention), the state
+// the sample ends in must equal rng_skip_sample(start, v) where v is the number of path
+// vertices (SceneDistribution::sample calls) of that sample.  stats: [0] samples, [1] states
+// that differ, [2] samples with v == ray_depth (the runahead's prediction).
+extern "C" void kh_skip_check(const rt_scene_view *v, int spp, int64_t n, const int64_t *pix, uint64_t *stats) {
+    rtd::DevScene sc = make(v);
+    uint64_t tot = 0, bad = 0, full = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : tot, bad, full)
+    for (int64_t q = 0; q < n; ++q) {
+        const int i = (int)(pix[q] % v->width), j = (int)(pix[q] / v->width);
+        const uint32_t seed = (uint32_t)(j * v->width + i) % 2147483647u;
+        rtd::Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
+        rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
+        for (int s = 0; s < spp; ++s) {
+            const rtd::Rng start = rng;
+            const float ox = rtd::rng_offset(rng), oy = rtd::rng_offset(rng);
+            rtd::Ray r = rtd::camera_ray(sc, i, j, ox, oy);
+            rtd::PathRec P;
+            int nv = 0, power = sc.ray_depth;
+            while (power > 0) {   // trace_sample (rt_path.h), keeping the vertex count
+                power -= 1;
+                rtd::Hit hit;
+                const bool ok = rtd::closest_hit<false>(sc, r, hit, cnt);
+                if (!(ok && hit.t < sc.max_distance)) break;
+                if (!rtd::shade_hit<false>(sc, r, hit, rng, cnt, P, nv)) break;
+            }
+            rtd::Rng pred = start;
+            rtd::rng_skip_sample(pred, nv, sc.n_lights);
+            ++tot;
+            full += nv == sc.ray_depth;
+            uint32_t a, b;
+            std::memcpy(&a, &pred.saved, 4);
+            std::memcpy(&b, &rng.saved, 4);
+            bad += !(pred.x == rng.x && pred.saved_avail == rng.saved_avail && a == b);
+        }
+    }
+    stats[0] = tot;
+    stats[1] = bad;
+    stats[2] = full;
 }
 
 // box_pair_hit (rt_wavefront.h) against box_hit_pt on each box of the pair, over `n`

@@ -61,6 +61,43 @@ def test_loader_path_matches_reference(gpu, name, w, h, s):
     assert st["rays"] == int(g["counters"][0]) and st["aabb_tests"] == int(g["counters"][1])
 
 
+@pytest.mark.parametrize("name,w,h,s", CASES)
+def test_runahead_matches_reference(gpu, name, w, h, s):
+    """Speculative sample runahead (default for non-counting parity renders; rt_mega.h
+    spec_manage): the whole frame and its 8 row-block shards (more lanes than pixels, so
+    every wave is in its tail from its first claim) against the reference's sums, and the
+    same frame with the runahead off."""
+    scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
+    ref = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["sums"].reshape(h, w, 3)
+    full, _ = scene.render_sums(s)
+    assert np.array_equal(rtref.bits(full), rtref.bits(ref))
+    off, _ = scene.render_sums(s, runahead=False)
+    assert np.array_equal(rtref.bits(off), rtref.bits(ref))
+    frame = np.zeros_like(full)
+    for rank in range(8):
+        rows = gpu.shard_rows(h, rank, 8, 8)
+        if len(rows):
+            frame[rows] = scene.render_sums(s, rank=rank, world=8)[0]
+    assert np.array_equal(rtref.bits(frame), rtref.bits(ref))
+
+
+def test_runahead_long_chains_vs_oracle(gpu, oracle):
+    """Runahead over 128-sample chains (many confirmations and invalidations per pixel) on
+    sponza_mini: runahead on = off, and sampled pixels = the CPU oracle."""
+    w, h, s = 64, 36, 128
+    scene = gpu.Scene.load(rtref.scene_path("sponza_mini"), w, h, s)
+    on, _ = scene.render_sums(s, rank=1, world=2)
+    off, _ = scene.render_sums(s, rank=1, world=2, runahead=False)
+    assert np.array_equal(rtref.bits(on), rtref.bits(off))
+    rows = gpu.shard_rows(h, 1, 2, 8)
+    arrays = scene.view()
+    rng = np.random.default_rng(13)
+    for k in rng.choice(len(rows) * w, 12, replace=False):
+        p = int(rows[k // w]) * w + int(k % w)
+        ref, _, _ = oracle.render(arrays, s, p, p + 1, threads=1)
+        assert np.array_equal(rtref.bits(on[k // w, k % w]), rtref.bits(ref[0])), f"pixel {p}"
+
+
 @pytest.mark.parametrize("name", ["cornell", "cornell_blob", "practice6_1", "sponza_mini"])
 def test_rays_match_reference(gpu, name):
     g = rtref.golden(f"{name}_rays.rtd")

@@ -145,6 +145,51 @@ def test_lane_resident_emulation(rt, kh, name, w, h, s, waves, shade_min):
     assert list(cnt[:6]) == list(cnt_want)
 
 
+@pytest.mark.parametrize("name,w,h,s,waves,world", [("cornell_blob", 48, 48, 4, 2, 1), ("sponza_mini", 64, 36, 4, 3, 1),
+                                                    ("cornell", 33, 17, 3, 1, 1), ("practice6_1", 256, 256, 4, 40, 1),
+                                                    ("sponza_mini", 64, 36, 4, 40, 1), ("sponza_mini", 64, 36, 4, 2, 3)])
+def test_lane_resident_runahead_emulation(rt, kh, name, w, h, s, waves, world):
+    """Speculative sample runahead (rt_mega.h spec_*): once the pixel queue is empty a wave's
+    idle lanes run later samples of its unfinished pixels from predicted start states, and
+    only results whose start state is proven are added.  Bit-exact sums, with the tail
+    reached late (few waves) and at once (more lanes than pixels), and on row-block shards."""
+    want, _ = _golden(name, w, h, s)
+    want = want.reshape(h, w, 3)
+    v, keep = _view(rt, name, w, h, s)
+    kh.kh_render_mega_spec.argtypes = kh.kh_render_mega.argtypes
+    kh.kh_render_mega_spec.restype = ctypes.c_int
+    for rank in range(world):
+        rows = rt.shard_rows(h, rank, world, 8)
+        out = np.zeros((len(rows) * w, 3), np.float32)
+        cnt = np.zeros(7, np.uint64)
+        assert kh.kh_render_mega_spec(ctypes.addressof(v), s, rank, world, 8, waves, 48, None, out.ctypes.data,
+                                      cnt.ctypes.data) == 0
+        assert np.array_equal(rtref.bits(out), rtref.bits(want[rows].reshape(-1, 3)))
+
+
+@pytest.mark.parametrize("name,w,h,s,waves", [("sponza_mini", 32, 18, 48, 4), ("cornell_blob", 24, 24, 64, 6)])
+def test_lane_resident_runahead_long_chains(rt, kh, name, w, h, s, waves):
+    """Runahead over long sample chains (48-64 spp, many confirmations and invalidations per
+    pixel) against the plain per-pixel schedule (rt_path.h render_pixel, pinned to the
+    reference by test_pixel_schedule_matches_reference)."""
+    v, keep = _view(rt, name, w, h, s)
+    want = np.zeros((h * w, 3), np.float32)
+    kh.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
+    kh.kh_render_mega_spec.argtypes = kh.kh_render_mega.argtypes
+    kh.kh_render_mega_spec.restype = ctypes.c_int
+    kh.kh_spec_stats.argtypes = [ctypes.c_void_p]
+    out = np.zeros((h * w, 3), np.float32)
+    stats = np.zeros(5, np.uint64)
+    kh.kh_spec_stats(stats.ctypes.data)
+    assert kh.kh_render_mega_spec(ctypes.addressof(v), s, 0, 1, 8, waves, 48, None, out.ctypes.data,
+                                  np.zeros(7, np.uint64).ctypes.data) == 0
+    kh.kh_spec_stats(stats.ctypes.data)
+    print(f"management passes {stats[0]}, frontier jobs {stats[1]}, runahead jobs {stats[2]}, added {stats[3]}, "
+          f"invalidations {stats[4]}")
+    assert stats[1] > 0 and stats[2] > 0 and stats[3] > stats[1]   # some runahead jobs were added
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
+
+
 @pytest.mark.parametrize("name,w,h,s,waves", [("cornell_blob", 48, 48, 4, 2), ("sponza_mini", 64, 36, 4, 3)])
 def test_lane_resident_any_pixel_order(rt, kh, name, w, h, s, waves):
     """The ordered render (rt_device.hip launch_order: queue item p renders pixel order[p])
@@ -198,3 +243,22 @@ def test_box_pair_matches_single_box_test(kh):
     primitive.cpp:146-208, restated op for op) on 4 M random cases rich in special values:
     signed zeros, infinities, NaN, flat and inverted boxes, planes through the origin."""
     assert kh.kh_box_pair_check(4_000_000, 7) == 0
+
+
+@pytest.mark.parametrize("name,w,h", [("cornell", 64, 64), ("cornell_blob", 48, 48), ("practice6_1", 64, 64),
+                                      ("sponza_mini", 64, 36)])
+def test_runahead_state_prediction(rt, kh, name, w, h):
+    """The speculative runahead's prediction (rt_path.h rng_skip_sample): the RNG state a
+    sample ends in is a function of its start state and its path's vertex count alone, so
+    skipping the draws of v vertices reproduces it exactly.  Checked on every sample of 256
+    pixels at 64 spp (parity RNG convention); the runahead itself still compares states
+    before it uses a speculative result (rt_mega.h spec_manage)."""
+    v, keep = _view(rt, name, w, h, 64)
+    rng = np.random.default_rng(5)
+    pix = np.ascontiguousarray(rng.choice(w * h, 256, replace=False), np.int64)
+    stats = np.zeros(3, np.uint64)
+    kh.kh_skip_check.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    kh.kh_skip_check(ctypes.addressof(v), 64, len(pix), pix.ctypes.data, stats.ctypes.data)
+    assert stats[0] == 256 * 64
+    assert stats[1] == 0, f"{stats[1]} of {stats[0]} sample end states differ from the prediction"
+    assert stats[2] > 0
