@@ -973,8 +973,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipStreamSynchronize(stream));
                 std::fprintf(stderr, "[mega prof] runahead: tail waves=%llu passes/tail wave=%.1f cycles/pass=%.0f "
                              "cycles in passes/wave=%.3g frontier jobs=%llu runahead jobs=%llu added=%llu "
-                             "invalidations=%llu\n", sp[7], sp[7] ? (double)sp[0] / sp[7] : 0.0,
-                             sp[0] ? (double)sp[1] / sp[0] : 0.0, (double)sp[1] / pf[7], sp[2], sp[3], sp[4], sp[6]);
+                             "runahead jobs proven=%llu invalidations=%llu\n", sp[7], sp[7] ? (double)sp[0] / sp[7] : 0.0,
+                             sp[0] ? (double)sp[1] / sp[0] : 0.0, (double)sp[1] / pf[7], sp[2], sp[3], sp[4], sp[5], sp[6]);
             }
 #endif
         }

@@ -678,6 +678,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                 unsigned long long tb = tab >> 6;   // table slots 1.. -> 0..
                 const V3 sum = rtv::add(rs.get(lane), c0);
                 const bool keep = (m & kRecXf) && n > f && rng_same(y1, e0);
+                RT_SPEC_STAT(5, keep ? 1 : 0);
                 RT_SPEC_STAT(4, 1);
                 if (!keep && n > f) {   // the runahead past f started from another state
                     re.put(lane, re.get(lane) + 1u);

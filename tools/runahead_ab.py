@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--worlds", default="8", help="comma-separated N of the N-way splits to time")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--off", type=int, default=1, help="also time with the runahead off")
+    ap.add_argument("--max-ranks", type=int, default=0, help="time only the first ranks of each split (0 = all)")
     args = ap.parse_args()
     rt = bench.import_pkg()
     path = bench.load_scenes_module().ensure_scene(args.scene, os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes"))
@@ -46,7 +47,7 @@ def main():
         tag = "on" if on else "off"
         res[f"full_ms_{tag}"] = round(t(1, 0, args.steps, on), 1)
         for world in [int(x) for x in args.worlds.split(",")]:
-            sh = [t(world, r, 1, on) for r in range(world)]
+            sh = [t(world, r, 1, on) for r in range(min(world, args.max_ranks or world))]
             res[f"shard{world}_ms_{tag}"] = [round(x, 1) for x in sh]
             res[f"shard{world}_max_ms_{tag}"] = round(max(sh), 1)
             res[f"speedup{world}_{tag}"] = round(res[f"full_ms_{tag}"] / max(sh), 3)
