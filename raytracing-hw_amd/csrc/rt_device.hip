@@ -184,6 +184,10 @@ __global__ void __launch_bounds__(256) rt_finish_kernel(const float *sum, long l
 // [6] sum of traversing lanes over traversal iterations [7] waves
 __device__ unsigned long long g_mega_prof[8];
 __device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT_PROF_SEG)
+// per-wave start and end (wall_clock64, 100 MHz): the distribution of wave finish times
+constexpr int kProfWaves = 16384;
+__device__ unsigned long long g_wave_t[2 * kProfWaves];
+__device__ unsigned int g_wave_n;
 #endif
 // FAST (RT_FLAG_FAST): queue items are (chunk, pixel) work units of `cs`
 // samples with per-sample Philox seeds; `out` is then the chunk-major partial buffer that
@@ -223,6 +227,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
     __syncthreads();
     long long tp = clock64();
+    const unsigned long long wt0 = wall_clock64();
 #endif
     for (;;) {
         if (!exhausted) {   // lanes without work take the next items (one atomic per wave)
@@ -303,6 +308,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     if (lane == 0) {
         for (int k = 0; k < 7; ++k) atomicAdd(&g_mega_prof[k], pf[k]);
         atomicAdd(&g_mega_prof[7], 1ull);
+        const unsigned wi = atomicAdd(&g_wave_n, 1u);
+        if (wi < (unsigned)kProfWaves) {
+            g_wave_t[2 * wi] = wt0;
+            g_wave_t[2 * wi + 1] = wall_clock64();
+        }
     }
     __syncthreads();
     if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
@@ -937,6 +947,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(rtd::g_spec_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
@@ -968,6 +979,25 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                              "normal=%.0f mr=%.0f sample=%.0f pdf=%.0f base+brdf=%.0f\n",
                              (double)sg[0] / pf[3], (double)sg[1] / pf[3], (double)sg[2] / pf[3],
                              (double)sg[3] / pf[3], (double)sg[4] / pf[3], (double)sg[5] / pf[3]);
+                {   // wave finish times relative to the first wave start: percentiles (ms)
+                    unsigned nw = 0;
+                    HIP_TRY(hipMemcpyFromSymbolAsync(&nw, HIP_SYMBOL(g_wave_n), sizeof nw, 0, hipMemcpyDeviceToHost, stream));
+                    HIP_TRY(hipStreamSynchronize(stream));
+                    nw = std::min<unsigned>(nw, (unsigned)kProfWaves);
+                    std::vector<unsigned long long> wt(2 * (size_t)nw);
+                    if (nw) HIP_TRY(hipMemcpyFromSymbolAsync(wt.data(), HIP_SYMBOL(g_wave_t), wt.size() * 8, 0, hipMemcpyDeviceToHost, stream));
+                    HIP_TRY(hipStreamSynchronize(stream));
+                    if (nw) {
+                        unsigned long long t0 = ~0ull;
+                        std::vector<double> ends(nw);
+                        for (unsigned i = 0; i < nw; ++i) t0 = std::min(t0, wt[2 * i]);
+                        for (unsigned i = 0; i < nw; ++i) ends[i] = (double)(wt[2 * i + 1] - t0) / 1e5;
+                        std::sort(ends.begin(), ends.end());
+                        std::fprintf(stderr, "[mega prof] wave end ms: p10=%.1f p25=%.1f p50=%.1f p75=%.1f p90=%.1f p99=%.1f max=%.1f\n",
+                                     ends[nw / 10], ends[nw / 4], ends[nw / 2], ends[3 * nw / 4], ends[9 * nw / 10],
+                                     ends[99 * (size_t)nw / 100], ends[nw - 1]);
+                    }
+                }
                 unsigned long long sp[8];
                 HIP_TRY(hipMemcpyFromSymbolAsync(sp, HIP_SYMBOL(rtd::g_spec_prof), sizeof sp, 0, hipMemcpyDeviceToHost, stream));
                 HIP_TRY(hipStreamSynchronize(stream));

@@ -202,7 +202,7 @@ template <bool COUNT, bool FAST = false, class Stack>
 __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
                                            Counters &cnt, bool tail = false) {
-    LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
+    LaneRec P{st.rec_ab, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     const Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
     bool next = false;
@@ -299,7 +299,7 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
                                                  const WfState &st, int spp, float *out, unsigned *cost,
                                                  const NodeRec &root, Stack &stk, Counters &cnt) {
     const long long slot = mega_slot();
-    LaneRec P{st.rec_ab, st.rec_ab + st.lanes * st.D, st.rec_c, slot, st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
+    LaneRec P{st.rec_ab, st.rec_c, slot, st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     float4 *mid = st.mid + slot;
     const long long ln = st.lanes;
     LaneCtr c = lane_ctr(L);

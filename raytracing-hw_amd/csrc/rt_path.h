@@ -703,14 +703,17 @@ struct AosRec {
 };
 
 // Vertex records of the lane-resident kernel, indexed by the lane's slot (its global thread
-// index) rather than by pixel: vertex k of slot i at k * lanes + i, in two float4 planes
-// (A: emission + coefficient, B: BRDF factor + cosine) and one float plane (alpha).  The
-// footprint is lanes x depth x 36 B (70 MB at 1080p, inside the 256 MB Infinity Cache)
-// instead of pixels x depth x 36 B, and a wave's lanes writing the same vertex index write
-// one contiguous 1-KB run per plane.
+// index) rather than by pixel, so the footprint is lanes x depth, not pixels x depth.
+// Vertex k of slot i is one 32-byte sector, R[2 (k * lanes + i)] = (coeff, m.xyz) and
+// R[... + 1] = (cos, e.xyz), written by the lane in two adjacent 16-byte stores; the path's
+// last vertex writes only its emission half.  The material alpha (1 for every opaque
+// material) is stored in its own plane only where it is not 1, which the sign bit of coeff
+// marks (coeff = 1 / pdf > 0, so the bit is free).  Round 2 kept (e, coeff), (m, cos) and
+// alpha in three planes: each vertex touched three sectors, and the records were 79% of
+// the kernel's HBM writes (profiles/r02e_record_layout_ab.jsonl).
 struct LaneRec {
-    float4 *A, *B;
-    float *c;
+    float4 *R;
+    float *al;
     long long i, lanes;
     V3 e;
     int ek;
@@ -718,40 +721,42 @@ struct LaneRec {
     __device__ __forceinline__ long long v(int k) const { return (long long)k * lanes + i; }
     __device__ __forceinline__ void set_e(int k, V3 x) { e = x; ek = k; pending = true; }
     __device__ __forceinline__ void set_brdf(int k, V3 mm, float cf, float cs, float a) {
-        A[v(k)] = make_float4(e.x, e.y, e.z, cf);
-        B[v(k)] = make_float4(mm.x, mm.y, mm.z, cs);
-        c[v(k)] = a;
+        const bool one = __float_as_uint(a) == 0x3f800000u;
+        R[2 * v(k)] = make_float4(__uint_as_float(__float_as_uint(cf) | (one ? 0u : 0x80000000u)), mm.x, mm.y, mm.z);
+        R[2 * v(k) + 1] = make_float4(cs, e.x, e.y, e.z);
+        if (!one) al[v(k)] = a;
         pending = false;
     }
     __device__ __forceinline__ void flush_e() {
-        if (pending) A[v(ek)] = make_float4(e.x, e.y, e.z, 0.f);
+        if (pending) R[2 * v(ek) + 1] = make_float4(0.f, e.x, e.y, e.z);
         pending = false;
     }
-    __device__ __forceinline__ V3 get_e(int k) const { const float4 a = A[v(k)]; return V3{a.x, a.y, a.z}; }
+    __device__ __forceinline__ V3 get_e(int k) const { const float4 b = R[2 * v(k) + 1]; return V3{b.y, b.z, b.w}; }
 };
-// fold_path over LaneRec: the backward recurrence, records read four vertices at a time.
+// fold_path over LaneRec: the backward recurrence, records read four vertices at a time
+// (alpha only for the vertices that stored one).
 __device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv) {
     if (nv == 0) return V3{0.f, 0.f, 0.f};
-    const float4 last = P.A[P.v(nv - 1)];
-    V3 c{last.x, last.y, last.z};
+    const float4 last = P.R[2 * P.v(nv - 1) + 1];
+    V3 c{last.y, last.z, last.w};
     for (int hi = nv - 2; hi >= 0; hi -= 4) {
         float4 A[4], B[4];
-        float C[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int k = hi - j >= 0 ? hi - j : 0;
-            A[j] = P.A[P.v(k)];
-            B[j] = P.B[P.v(k)];
-            C[j] = P.c[P.v(k)];
+            A[j] = P.R[2 * P.v(k)];
+            B[j] = P.R[2 * P.v(k) + 1];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (hi - j < 0) break;
-            V3 x = rtv::mul(c, A[j].w);
-            x = rtv::mulv(x, V3{B[j].x, B[j].y, B[j].z});
-            x = rtv::mul(x, B[j].w);
-            x = rtv::mul(x, C[j]);
-            c = rtv::add(V3{A[j].x, A[j].y, A[j].z}, x);
+            const uint32_t cb = __float_as_uint(A[j].x);
+            const float alpha = (cb >> 31) ? P.al[P.v(hi - j)] : 1.f;
+            V3 x = rtv::mul(c, __uint_as_float(cb & 0x7fffffffu));
+            x = rtv::mulv(x, V3{A[j].y, A[j].z, A[j].w});
+            x = rtv::mul(x, B[j].x);
+            x = rtv::mul(x, alpha);
+            c = rtv::add(V3{B[j].y, B[j].z, B[j].w}, x);
         }
     }
     return c;

@@ -33,8 +33,8 @@ struct WfState {
     long long n;      // path slots (= pixels of the shard)
     int D;            // vertex records per slot (= ray_depth)
     float4 *st;       // 2 per slot: (rng state bits, normal cache, meta bits, 0), (pixel sum, 0)
-    float4 *rec_ab;   // AosRec: 2 per slot and vertex
-    float *rec_c;     //         1 per slot and vertex
+    float4 *rec_ab;   // AosRec: 2 per slot and vertex; LaneRec: 2 per vertex and lane slot
+    float *rec_c;     //         1 per slot and vertex; LaneRec: alpha per vertex and lane slot
     long long lanes;  // lane-resident kernel: lane slots (LaneRec stride; rt_path.h)
     float4 *mid;      // light-split kernel: shading state across the light walk, 5 per lane slot (rt_mega.h)
 };

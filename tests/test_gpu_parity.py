@@ -98,6 +98,22 @@ def test_runahead_long_chains_vs_oracle(gpu, oracle):
         assert np.array_equal(rtref.bits(on[k // w, k % w]), rtref.bits(ref[0])), f"pixel {p}"
 
 
+def test_translucent_materials_vs_oracle(gpu, oracle):
+    """Materials with alpha != 1 (scene.cpp:151; every fixture is opaque): the lane-resident
+    kernel stores alpha only for such vertices (rt_path.h LaneRec).  Both kernels, with and
+    without runahead, against the CPU oracle on the same arrays."""
+    name, w, h, s = "sponza_mini", 48, 27, 6
+    a = rtref.ref_arrays(gpu, name, w, h, s)
+    a["mesh_f"] = a["mesh_f"].copy()
+    a["mesh_f"][::2, 8] = np.float32(0.37)
+    a["mesh_f"][1::4, 8] = np.float32(1.0000001)
+    scene = gpu.Scene.from_view(a)
+    ref, _, _ = oracle.render(a, s)
+    for kw in ({}, {"runahead": False}, {"kernel": 4}, {"count": True}):
+        out, _ = _sums(scene, s, **kw)
+        assert np.array_equal(rtref.bits(out), rtref.bits(ref)), kw
+
+
 @pytest.mark.parametrize("name", ["cornell", "cornell_blob", "practice6_1", "sponza_mini"])
 def test_rays_match_reference(gpu, name):
     g = rtref.golden(f"{name}_rays.rtd")

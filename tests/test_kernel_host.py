@@ -262,3 +262,25 @@ def test_runahead_state_prediction(rt, kh, name, w, h):
     assert stats[0] == 256 * 64
     assert stats[1] == 0, f"{stats[1]} of {stats[0]} sample end states differ from the prediction"
     assert stats[2] > 0
+
+
+def test_lane_resident_translucent_materials(rt, kh):
+    """Materials with alpha != 1 (the reference multiplies the bounce by material.alpha,
+    scene.cpp:151; every fixture is opaque): the lane-resident kernel stores alpha only for
+    such vertices (rt_path.h LaneRec), with and without runahead, against the per-pixel
+    schedule on the same arrays."""
+    name, w, h, s = "sponza_mini", 48, 27, 6
+    a = rtref.ref_arrays(rt, name, w, h, s)
+    a["mesh_f"] = a["mesh_f"].copy()
+    a["mesh_f"][::2, 8] = np.float32(0.37)
+    a["mesh_f"][1::4, 8] = np.float32(1.0000001)
+    v, keep = rt.make_view(a)
+    want = np.zeros((h * w, 3), np.float32)
+    kh.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
+    kh.kh_render_mega_spec.argtypes = kh.kh_render_mega.argtypes
+    kh.kh_render_mega_spec.restype = ctypes.c_int
+    for fn in (kh.kh_render_mega, kh.kh_render_mega_spec):
+        out = np.zeros((h * w, 3), np.float32)
+        assert fn(ctypes.addressof(v), s, 0, 1, 8, 3, 48, None, out.ctypes.data, np.zeros(7, np.uint64).ctypes.data) == 0
+        assert np.array_equal(rtref.bits(out), rtref.bits(want))
+    assert not np.array_equal(want, 0)
