@@ -206,7 +206,8 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
     const Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
     bool next = false;
-    if (h.prim >= 0 && h.t < sc.max_distance) {
+    const bool shaded = h.prim >= 0 && h.t < sc.max_distance;
+    if (shaded) {
         Rng rng = lane_rng(L);
         const bool cont = shade_hit<COUNT>(sc, L.r, h, rng, cnt, P, c.nv, stk);   // (stack free: T.sp == 0)
         lane_rng_set(L, rng);
@@ -215,17 +216,18 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
             next = true;
         }
     }
-    P.flush_e();
+    // (no flush_e: a continued vertex has its record; a path that ends at the vertex shaded
+    // here folds from its emission in registers)
     if (next) {
         lane_ctr_set(L, c);
         mega_begin<COUNT>(L, root, cnt);
         return;
     }
     if (!COUNT && !FAST && tail) {   // runahead job: colour of sample c.s, end state in the RNG slot
-        spec_job_end(L, sc, g, st, spp, out, root, fold_path(P, c.nv), c);
+        spec_job_end(L, sc, g, st, spp, out, root, fold_path(P, c.nv, shaded), c);
         return;
     }
-    const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv));
+    const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv, shaded));
     lane_sum_set(L, sm);
     if (++c.s == (FAST ? L.send : spp)) {
         const long long o = FAST ? L.dst : L.pix;

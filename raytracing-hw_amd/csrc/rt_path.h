@@ -734,11 +734,15 @@ struct LaneRec {
     __device__ __forceinline__ V3 get_e(int k) const { const float4 b = R[2 * v(k) + 1]; return V3{b.y, b.z, b.w}; }
 };
 // fold_path over LaneRec: the backward recurrence, records read four vertices at a time
-// (alpha only for the vertices that stored one).
-__device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv) {
+// (alpha only for the vertices that stored one).  last_here: the last vertex was shaded in
+// this call, so its emission is still P.e (the path's end never writes it to memory).
+__device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv, bool last_here = false) {
     if (nv == 0) return V3{0.f, 0.f, 0.f};
-    const float4 last = P.R[2 * P.v(nv - 1) + 1];
-    V3 c{last.y, last.z, last.w};
+    V3 c = P.e;
+    if (!last_here) {
+        const float4 last = P.R[2 * P.v(nv - 1) + 1];
+        c = V3{last.y, last.z, last.w};
+    }
     for (int hi = nv - 2; hi >= 0; hi -= 4) {
         float4 A[4], B[4];
 #pragma unroll
