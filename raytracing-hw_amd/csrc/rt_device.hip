@@ -40,8 +40,18 @@ using rtd::ShardGeom;
 using rtd::shard_row;
 
 // Tuned constants of the default kernel (measured values in DESIGN.md §5-6).
-constexpr int kMegaWpe = 5;          // waves per SIMD the register allocation targets (96 VGPRs)
-constexpr int kShadeMin = 48;        // a wave shades once this many lanes are READY (or none traverses)
+#ifndef RT_MEGA_WPE
+#define RT_MEGA_WPE 5
+#endif
+constexpr int kMegaWpe = RT_MEGA_WPE;   // waves per SIMD the register allocation targets (96 VGPRs)
+// The runahead instantiation runs shards of at most one pixel per lane, which the
+// five-wave grid does not fill anyway (an 8-way shard of the headline: 1013 blocks, 4
+// waves per SIMD): 128 VGPRs instead of 96 keep its management pass from spilling the loop.
+constexpr int kMegaWpeSpec = 4;
+#ifndef RT_SHADE_MIN
+#define RT_SHADE_MIN 48
+#endif
+constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -200,7 +210,7 @@ __device__ unsigned int g_wave_n;
 // tail and runs speculative sample runahead (rt_mega.h spec_manage) on its idle lanes.  A
 // separate instantiation, so the kernel without it keeps its own register allocation.
 template <bool COUNT, bool FAST = false, bool LSPLIT = false, bool SPEC = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMegaWpe, 8)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPEC ? kMegaWpeSpec : kMegaWpe, 8)))
 rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
                unsigned long long *queue, const int *order, unsigned *cost, int cs) {
     constexpr bool kSpec = SPEC && !COUNT && !FAST && !LSPLIT;
