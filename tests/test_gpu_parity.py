@@ -81,6 +81,23 @@ def test_runahead_matches_reference(gpu, name, w, h, s):
     assert np.array_equal(rtref.bits(frame), rtref.bits(ref))
 
 
+@pytest.mark.parametrize("spp", [1, 2, 5])
+def test_runahead_short_chains_vs_oracle(gpu, oracle, spp):
+    """Runahead with chains shorter than its window (1, 2 and 5 samples per pixel), whole
+    frame and 8-way shards, against the CPU oracle."""
+    w, h = 33, 17
+    scene = gpu.Scene.load(rtref.scene_path("cornell_blob"), w, h, spp)
+    ref, _, _ = oracle.render(scene.view(), spp)
+    ref = ref.reshape(h, w, 3)
+    full, _ = scene.render_sums(spp)
+    assert np.array_equal(rtref.bits(full), rtref.bits(ref))
+    for rank in range(8):
+        rows = gpu.shard_rows(h, rank, 8, 8)
+        if len(rows):
+            part, _ = scene.render_sums(spp, rank=rank, world=8)
+            assert np.array_equal(rtref.bits(part), rtref.bits(ref[rows]))
+
+
 def test_runahead_long_chains_vs_oracle(gpu, oracle):
     """Runahead over 128-sample chains (many confirmations and invalidations per pixel) on
     sponza_mini: runahead on = off, and sampled pixels = the CPU oracle."""
