@@ -131,6 +131,21 @@ def test_translucent_materials_vs_oracle(gpu, oracle):
         assert np.array_equal(rtref.bits(out), rtref.bits(ref)), kw
 
 
+def test_scene_without_lights_vs_oracle(gpu, oracle):
+    """No emissive triangles (SceneDistribution picks between cosine and VNDF only,
+    random.cpp:196-199; the pdf has no light term): both kernels, with and without runahead,
+    against the CPU oracle."""
+    name, w, h, s = "cornell_blob", 40, 40, 12
+    a = rtref.ref_arrays(gpu, name, w, h, s)
+    a["light"] = np.zeros((0, 16), np.float32)
+    a["light_node"] = np.zeros((0, 8), np.float32)
+    scene = gpu.Scene.from_view(a)
+    ref, _, _ = oracle.render(a, s)
+    for kw in ({}, {"runahead": False}, {"kernel": 4}):
+        out, _ = _sums(scene, s, **kw)
+        assert np.array_equal(rtref.bits(out), rtref.bits(ref)), kw
+
+
 @pytest.mark.parametrize("name", ["cornell", "cornell_blob", "practice6_1", "sponza_mini"])
 def test_rays_match_reference(gpu, name):
     g = rtref.golden(f"{name}_rays.rtd")

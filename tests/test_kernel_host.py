@@ -284,3 +284,28 @@ def test_lane_resident_translucent_materials(rt, kh):
         assert fn(ctypes.addressof(v), s, 0, 1, 8, 3, 48, None, out.ctypes.data, np.zeros(7, np.uint64).ctypes.data) == 0
         assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert not np.array_equal(want, 0)
+
+
+def test_runahead_without_lights(rt, kh):
+    """A scene without emissive triangles (SceneDistribution::sample then picks between
+    cosine and VNDF only, random.cpp:196-199): the runahead's state prediction and the
+    runahead schedule against the per-pixel schedule."""
+    name, w, h, s = "cornell_blob", 40, 40, 24
+    a = rtref.ref_arrays(rt, name, w, h, s)
+    a["light"] = np.zeros((0, 16), np.float32)
+    a["light_node"] = np.zeros((0, 8), np.float32)
+    v, keep = rt.make_view(a)
+    assert v.n_lights == 0
+    stats = np.zeros(3, np.uint64)
+    pix = np.arange(w * h, dtype=np.int64)
+    kh.kh_skip_check.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    kh.kh_skip_check(ctypes.addressof(v), s, len(pix), pix.ctypes.data, stats.ctypes.data)
+    assert stats[0] == w * h * s and stats[1] == 0 and stats[2] > 0
+    want = np.zeros((h * w, 3), np.float32)
+    kh.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
+    kh.kh_render_mega_spec.argtypes = kh.kh_render_mega.argtypes
+    kh.kh_render_mega_spec.restype = ctypes.c_int
+    out = np.zeros((h * w, 3), np.float32)
+    assert kh.kh_render_mega_spec(ctypes.addressof(v), s, 0, 1, 8, 5, 48, None, out.ctypes.data,
+                                  np.zeros(7, np.uint64).ctypes.data) == 0
+    assert np.array_equal(rtref.bits(out), rtref.bits(want))
