@@ -216,8 +216,10 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
             next = true;
         }
     }
-    // (no flush_e: a continued vertex has its record; a path that ends at the vertex shaded
-    // here folds from its emission in registers)
+    // (parity: no flush_e; a continued vertex has its record, and a path that ends at the
+    // vertex shaded here folds from its emission in registers.  Fast mode writes it and folds
+    // from memory: keeping it live there made that instantiation spill 31 VGPRs instead of 22.)
+    if constexpr (FAST) P.flush_e();
     if (next) {
         lane_ctr_set(L, c);
         mega_begin<COUNT>(L, root, cnt);
@@ -227,7 +229,7 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
         spec_job_end(L, sc, g, st, spp, out, root, fold_path(P, c.nv, shaded), c);
         return;
     }
-    const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv, shaded));
+    const V3 sm = rtv::add(lane_sum(L), fold_path(P, c.nv, !FAST && shaded));
     lane_sum_set(L, sm);
     if (++c.s == (FAST ? L.send : spp)) {
         const long long o = FAST ? L.dst : L.pix;

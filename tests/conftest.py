@@ -14,6 +14,14 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def rt():
+    # On a GPU box torch must initialise its HIP runtime before librt_hw_amd.so is loaded
+    # (see test_gpu_parity.py), also when CPU tests that load the library run first.
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
+    except ImportError:
+        pass
     import rtref
     return rtref.package()
 
