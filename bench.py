@@ -33,6 +33,7 @@ cpu_baseline: the reference itself (oracle/_ref/ref_render, built from /root/ref
            when _ref is absent.
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -162,13 +163,30 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # RT_BENCH_SHARE_GPU=1: rehearsal of the N-rank logic on a one-GPU box (every rank on
+    # device 0, gloo collectives on host copies); its timings mean nothing
+    share = os.environ.get("RT_BENCH_SHARE_GPU") == "1"
+    dev = 0 if share else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def all_reduce(t, op):
+        if world == 1:
+            return
+        if share:
+            c = t.cpu()
+            dist.all_reduce(c, op=op)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=op)
 
     rt = import_pkg()
     scene_dir = os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes")
@@ -180,7 +198,7 @@ def main():
     W, H, S = args.width, args.height, args.spp
     t0 = time.time()
     scene = rt.Scene.load(path, W, H, S)
-    scene.upload(local)
+    scene.upload(dev)
     load_s = time.time() - t0
     n_tris = scene.view()["tri"].shape[0]
 
@@ -196,9 +214,12 @@ def main():
         # render the shard, finish it to 8 bits on the GPU (scene.cpp:54-64), gather the frame
         st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
                                  count=count, kernel=args.kernel, stats=True, kernel_times=not count, fast=fast,
-                                 fast_chunk=args.fast_chunk, device=local, natural_order=natural)
+                                 fast_chunk=args.fast_chunk, device=dev, natural_order=natural)
         rt.tonemap_device(out.data_ptr(), W, max_rows, S, rgb.data_ptr(), stream)
-        rtdist.gather_frame(rgb, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
+        if share and world > 1:
+            frame.copy_(rtdist.gather_frame(rgb.cpu(), H, W, rank, world, args.row_block))
+        else:
+            rtdist.gather_frame(rgb, H, W, rank, world, args.row_block, out=frame)   # RCCL all-gather (N > 1)
         return st
 
     def timed(n, **kw):
@@ -212,8 +233,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, dist.ReduceOp.MAX)
         return float(t.item()), sts
 
     # the very first frame of this scene on this device: nothing from an earlier render
@@ -240,6 +260,9 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    # digest of the gathered 8-bit frame (outside the timed region): the parity path is
+    # bit-exact whatever the sharding, so this must agree across --gpus 1/2/4/8 runs
+    digest = hashlib.sha1(frame.cpu().numpy().tobytes()).hexdigest()[:16] if rank == 0 else None
 
     natural_s = None
     if args.natural_steps > 0 and args.kernel == 0:
@@ -261,9 +284,8 @@ def main():
         barrier()
         t_fast = torch.tensor([time.perf_counter() - tf], dtype=torch.float64, device="cuda")
         r_fast = torch.tensor([float(fc["rays"])], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(t_fast, op=dist.ReduceOp.MAX)
-            dist.all_reduce(r_fast, op=dist.ReduceOp.SUM)
+        all_reduce(t_fast, dist.ReduceOp.MAX)
+        all_reduce(r_fast, dist.ReduceOp.SUM)
         fe, frays = float(t_fast.item()), float(r_fast.item())
         fast_line = {"value": round(frays * args.fast_steps / fe / 1e6, 3), "unit": "Mrays/s",
                      "ms_per_step": round(fe / args.fast_steps * 1e3, 3), "steps": args.fast_steps,
@@ -275,9 +297,8 @@ def main():
     keys = ["rays", "aabb_tests", "tri_tests", "light_queries", "light_aabb_tests", "light_tri_tests", "shading_hits"]
     local_counts = torch.tensor([counts[k] for k in keys], dtype=torch.float64, device="cuda")
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(local_counts, op=dist.ReduceOp.SUM)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    all_reduce(local_counts, dist.ReduceOp.SUM)
+    all_reduce(t, dist.ReduceOp.MAX)
     total = dict(zip(keys, local_counts.tolist()))
     elapsed = float(t.item())
 
@@ -339,7 +360,7 @@ def main():
                        "order_ms": round(float(np.mean(order_ms)), 3),
                        "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
                        "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
-                       "scene_load_s": round(load_s, 3)},
+                       "scene_load_s": round(load_s, 3), "frame_sha1": digest},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else int(traffic),

@@ -92,3 +92,56 @@ def test_gpu_fast_rejects_other_kernels(gpu):
     scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, "cornell", 16, 16, 2))
     with pytest.raises(gpu.RtError, match="kernel 0"):
         scene.render_sums(2, fast=True, kernel=4)
+
+
+
+def _tile_z(d, tile):
+    """Per-(tile, channel) z-scores of the mean of d (h, w, 3) over tile x tile blocks."""
+    h, w, _ = d.shape
+    zs = []
+    for y in range(0, h, tile):
+        for x in range(0, w, tile):
+            b = d[y:y + tile, x:x + tile].reshape(-1, 3)
+            se = b.std(0, ddof=1) / np.sqrt(len(b))
+            zs.append(np.abs(b.mean(0)) / np.maximum(se, 1e-12))
+    return np.array(zs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,w,h,s", [("cornell", 256, 256, 1024), ("sponza_mini", 256, 144, 512)])
+def test_gpu_fast_unbiased_and_same_distribution(gpu, name, w, h, s):
+    """Fast mode against the parity estimator (itself bit-exact with the reference).
+    A = parity's first s samples, B = its next s (sum(2s) - sum(s): the parity stream is
+    sequential per pixel, scene.cpp:31-44), F = fast mode's s samples, all per-pixel means.
+    Path-traced pixel means are heavy-tailed (a few fireflies hold most of the squared error),
+    so the statistics are robust ones, applied identically to both estimators:
+      * bias: per-pixel means capped at 4x the frame median (the same monotone map of two
+        estimators of one distribution has one expectation); frame and every 32x32 tile, per
+        channel, |mean(F - A)| within 4.5 standard errors;
+      * power: the frame statistic flags F scaled by 1.02 or 0.98 (a 2% bias does not pass);
+      * distribution: quantiles of |F - A| against those of |B - A| (independent estimates
+        with the reference's per-pixel spread): median and 90th within 5%, 99th within 13%.
+    Thresholds checked against the CPU restatement at these sizes (frame z <= 1.8, tile z
+    <= 2.9, 2% bias z >= 6.5, quantile ratios 0.99-1.05)."""
+    scene = gpu.Scene.load(rtref.scene_path(name), w, h, s)
+    a, _ = scene.render_sums(s)
+    a2, _ = scene.render_sums(2 * s)
+    f, _ = scene.render_sums(s, fast=True)
+    A = a.astype(np.float64) / s
+    B = (a2.astype(np.float64) - a.astype(np.float64)) / s
+    F = f.astype(np.float64) / s
+    assert np.isfinite(F).all() and (F >= 0).all()
+    cap = 4 * np.median(A)
+
+    def frame_z(x):
+        d = (np.minimum(x, cap) - np.minimum(A, cap)).reshape(-1, 3)
+        return np.abs(d.mean(0)) / (d.std(0, ddof=1) / np.sqrt(len(d)))
+
+    assert (frame_z(F) <= 4.5).all(), frame_z(F)
+    z = _tile_z(np.minimum(F, cap) - np.minimum(A, cap), 32)
+    assert z.max() <= 4.5, (z.max(), np.unravel_index(z.argmax(), z.shape))
+    assert (frame_z(1.02 * F) > 4.5).all() and (frame_z(0.98 * F) > 4.5).all(), \
+        (frame_z(1.02 * F), frame_z(0.98 * F))
+    for q, tol in [(50, 0.05), (90, 0.05), (99, 0.13)]:
+        r = np.percentile(np.abs(F - A), q) / np.percentile(np.abs(B - A), q)
+        assert abs(r - 1) <= tol, (q, r)
