@@ -308,6 +308,36 @@ extern "C" void kh_skip_check(const rt_scene_view *v, int spp, int64_t n, const 
     stats[2] = full;
 }
 
+// Per-sample vertex count and traversal cost of the listed pixels (parity RNG convention):
+// the data the runahead's prediction of v is measured on (tools/runahead_predict.py).
+// nv_out[q*spp + s] = vertices of sample s of pixel q, cost_out[q*spp + s] = its box + triangle tests.
+extern "C" void kh_v_trace(const rt_scene_view *v, int spp, int64_t n, const int64_t *pix, uint8_t *nv_out,
+                           uint32_t *cost_out) {
+    rtd::DevScene sc = make(v);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t q = 0; q < n; ++q) {
+        const int i = (int)(pix[q] % v->width), j = (int)(pix[q] / v->width);
+        const uint32_t seed = (uint32_t)(j * v->width + i) % 2147483647u;
+        rtd::Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
+        for (int s = 0; s < spp; ++s) {
+            rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
+            const float ox = rtd::rng_offset(rng), oy = rtd::rng_offset(rng);
+            rtd::Ray r = rtd::camera_ray(sc, i, j, ox, oy);
+            rtd::PathRec P;
+            int nv = 0, power = sc.ray_depth;
+            while (power > 0) {
+                power -= 1;
+                rtd::Hit hit;
+                const bool ok = rtd::closest_hit<true>(sc, r, hit, cnt);
+                if (!(ok && hit.t < sc.max_distance)) break;
+                if (!rtd::shade_hit<true>(sc, r, hit, rng, cnt, P, nv)) break;
+            }
+            nv_out[q * spp + s] = (uint8_t)nv;
+            cost_out[q * spp + s] = (uint32_t)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri);
+        }
+    }
+}
+
 // box_pair_hit (rt_wavefront.h) against box_hit_pt on each box of the pair, over `n`
 // random cases drawn from a small set of special values (planes through the origin,
 // signed zeros, infinities, NaN, inverted boxes) mixed with ordinary floats.  Returns the
