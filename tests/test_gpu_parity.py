@@ -236,6 +236,26 @@ def test_render_multi_matches_single_device(gpu):
         assert st["rays"] == int(rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["counters"][0])
 
 
+def test_concurrent_scenes_on_one_device(gpu):
+    """Two scene copies rendering at once on one device, each on its own stream with no wait
+    between the launches (include/rt_hw.h: only one render per (scene, device) may be in
+    flight; separate scenes share no device state): every frame equals the reference's."""
+    import torch
+    name, w, h, s = "sponza_mini", 64, 36, 4
+    ref = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["sums"].reshape(-1)
+    scenes = [gpu.Scene.load(rtref.scene_path(name), w, h, s) for _ in range(2)]
+    for sc in scenes:
+        sc.upload(0)
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.full((h * w * 3,), float("nan"), dtype=torch.float32, device="cuda") for _ in range(6)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        scenes[i % 2].render_device(o.data_ptr(), streams[i % 2].cuda_stream, spp=s, natural_order=(i % 3 == 2))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(rtref.bits(o.cpu().numpy()), rtref.bits(ref))
+
+
 def test_device_finish_matches_reference(gpu):
     """rt_tonemap_u8_device (scene.cpp:54-64 on the GPU) against the reference's own 8-bit
     finish of the golden sums (NaN, inf, negative, saturating values included) and against

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--off", type=int, default=1, help="also time with the runahead off")
     ap.add_argument("--max-ranks", type=int, default=0, help="time only the first ranks of each split (0 = all)")
+    ap.add_argument("--full", type=int, default=1, help="also time the whole frame on one GPU")
     args = ap.parse_args()
     rt = bench.import_pkg()
     path = bench.load_scenes_module().ensure_scene(args.scene, os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes"))
@@ -42,15 +43,21 @@ def main():
                                   runahead=on)["render_ms"] for _ in range(steps)]
         return min(ms)
 
-    t(1, 0, 1, True)   # warm
+    worlds = [int(x) for x in args.worlds.split(",")]
+    if args.full:
+        t(1, 0, 1, True)   # warm
+    else:
+        t(worlds[0], 0, 1, True)
     for on in ([True, False] if args.off else [True]):
         tag = "on" if on else "off"
-        res[f"full_ms_{tag}"] = round(t(1, 0, args.steps, on), 1)
-        for world in [int(x) for x in args.worlds.split(",")]:
+        if args.full:
+            res[f"full_ms_{tag}"] = round(t(1, 0, args.steps, on), 1)
+        for world in worlds:
             sh = [t(world, r, 1, on) for r in range(min(world, args.max_ranks or world))]
             res[f"shard{world}_ms_{tag}"] = [round(x, 1) for x in sh]
             res[f"shard{world}_max_ms_{tag}"] = round(max(sh), 1)
-            res[f"speedup{world}_{tag}"] = round(res[f"full_ms_{tag}"] / max(sh), 3)
+            if args.full:
+                res[f"speedup{world}_{tag}"] = round(res[f"full_ms_{tag}"] / max(sh), 3)
         print(json.dumps(res), flush=True)
 
 
