@@ -147,6 +147,8 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
 // by host loops over the wave's lanes where the kernel uses ballots (rt_mega.h spec_manage);
 // a non-counting render, as on the GPU.
 static uint64_t g_spec_passes = 0;   // management passes since the last kh_spec_stats
+static uint64_t g_rounds = 0;        // main-loop rounds (one iteration of every live wave) of the last render
+extern "C" uint64_t kh_rounds() { return g_rounds; }
 extern "C" void kh_spec_stats(uint64_t *out) {   // passes, frontier jobs, runahead jobs, added, invalidations
     out[0] = g_spec_passes;
     out[1] = rtd::g_spec_prof[2];
@@ -189,7 +191,9 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
     long long queue = 0;
     int live = waves;
+    g_rounds = 0;
     while (live > 0) {
+        ++g_rounds;
         for (int w = 0; w < waves; ++w) {
             if (done[w]) continue;
             rtd::MegaLane *W = &lanes[(size_t)w * 64];
