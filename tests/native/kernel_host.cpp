@@ -147,6 +147,8 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
 // by host loops over the wave's lanes where the kernel uses ballots (rt_mega.h spec_manage);
 // a non-counting render, as on the GPU.
 static uint64_t g_spec_passes = 0;   // management passes since the last kh_spec_stats
+static int g_static_per_wave = 0;    // > 0: no queue; wave w takes items [w*P, w*P+P) (study of spare lanes)
+extern "C" void kh_set_static_per_wave(int p) { g_static_per_wave = p; }
 static uint64_t g_rounds = 0;        // main-loop rounds (one iteration of every live wave) of the last render
 extern "C" uint64_t kh_rounds() { return g_rounds; }
 extern "C" void kh_spec_stats(uint64_t *out) {   // passes, frontier jobs, runahead jobs, added, invalidations
@@ -197,6 +199,13 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
         for (int w = 0; w < waves; ++w) {
             if (done[w]) continue;
             rtd::MegaLane *W = &lanes[(size_t)w * 64];
+            if (!exhausted[w] && g_static_per_wave > 0) {   // static allotment: wave w renders items [w*P, w*P+P)
+                for (int l = 0; l < 64 && l < g_static_per_wave; ++l) {
+                    const long long p = (long long)w * g_static_per_wave + l;
+                    if (p < n) rtd::mega_assign<!SPEC>(W[l], sc, g, order ? order[p] : (int)p, root, cnt);
+                }
+                exhausted[w] = 1;
+            }
             if (!exhausted[w]) {
                 uint64_t m = 0;
                 for (int l = 0; l < 64; ++l) if (W[l].pix < 0) m |= 1ull << l;
