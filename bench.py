@@ -355,7 +355,8 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "spp": S, "triangles": int(n_tris),
                        "kernel": {0: "lane-resident", 4: "wavefront"}[args.kernel],
                        "parallelism": f"pixel-rows x{world}",
-                       "pixel_order": "heaviest-first from a counting pre-pass inside each timed frame"
+                       "pixel_order": ("heaviest-first from a counting pre-pass inside each timed frame" if S >= 128
+                                       else "row-major (below 128 spp the library skips the pre-pass)")
                                       if args.kernel == 0 else "row-major",
                        "order_ms": round(float(np.mean(order_ms)), 3),
                        "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
@@ -375,7 +376,8 @@ def main():
             "natural_order": None if natural_s is None else {
                 "ms_per_step": round(natural_s / args.natural_steps * 1e3, 3), "steps": args.natural_steps,
                 "value": round(rays_per_frame * args.natural_steps / natural_s / 1e6, 3), "unit": "Mrays/s",
-                "note": "RT_FLAG_NATURAL_ORDER: row-major pixel order, no pre-pass (same bits)"},
+                "note": "RT_FLAG_NATURAL_ORDER: row-major pixel order, no pre-pass (same bits; the default "
+                        "below 128 spp)"},
             "fast_mode": fast_line,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -113,11 +113,14 @@ typedef struct {
  * walk as its own traversal state between two shading passes.  Same bits; measured slower
  * on every scene tried, so off by default. */
 #define RT_FLAG_LIGHT_SPLIT 4
-/* Parity mode renders pixels heaviest-first: a counting pre-pass of 1 sample per pixel
- * (its own Philox streams), a box filter, a radix sort and a spread over the waves, all
- * inside the call and inside render_ms.  This flag renders in row-major order instead (same
- * bits). */
+/* Parity mode at spp >= 128 renders pixels heaviest-first: a counting pre-pass of 1 sample
+ * per pixel (its own Philox streams), a box filter, a radix sort and a spread over the
+ * waves, all inside the call and inside render_ms.  Below 128 spp it renders in row-major
+ * order (the pre-pass would cost more than it gains).  NATURAL_ORDER always renders in
+ * row-major order, HEAVY_ORDER always builds the heaviest-first order; same bits either way,
+ * and the two flags exclude each other (RT_ERR_ARG). */
 #define RT_FLAG_NATURAL_ORDER 8
+#define RT_FLAG_HEAVY_ORDER 32
 /* Parity mode, once the pixel queue is empty, runs the next samples of a wave's unfinished
  * pixels on its idle lanes before their start state is known, and adds only those whose
  * start state is proven equal to the sequential chain's (rt_mega.h, speculative sample

@@ -67,6 +67,12 @@ constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes 
 #endif
 constexpr int kOrderSpp = RT_ORDER_SPP;        // samples per pixel of the counting pre-pass
 constexpr int kOrderRadius = RT_ORDER_RADIUS;  // box filter of the pre-pass costs ((2r+1)^2 pixels)
+// The pre-pass and sort cost about one sample per pixel, so below kOrderMinSpp the order
+// is not built unless asked for (RT_FLAG_HEAVY_ORDER): row-major measured faster there
+// (profiles/r02_configs.jsonl: C1 256x256x4 4.5 vs 5.0 ms, C2 512x512x64 17.7 vs 18.0 ms, C5
+// 3840x2160 at 16 spp 378 vs 397 ms; at 256 spp the order wins, C3 748 vs 779 ms, headline
+// 1357 vs 1393 ms).
+constexpr int kOrderMinSpp = 128;
 constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units per pixel
 #ifndef RT_SPEC_PIXELS_PER_LANE
 #define RT_SPEC_PIXELS_PER_LANE 1
@@ -885,6 +891,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
     if ((fast || (p->flags & RT_FLAG_LIGHT_SPLIT)) && p->kernel != RT_KERNEL_LANE)
         return rt_fail(RT_ERR_ARG, "rt_render: fast mode and the light-split kernel run on kernel 0 only");
     if (p->fast_chunk < 0) return rt_fail(RT_ERR_ARG, "rt_render: fast_chunk must be >= 0");
+    if ((p->flags & RT_FLAG_NATURAL_ORDER) && (p->flags & RT_FLAG_HEAVY_ORDER))
+        return rt_fail(RT_ERR_ARG, "rt_render: RT_FLAG_NATURAL_ORDER and RT_FLAG_HEAVY_ORDER exclude each other");
     if ((int64_t)s->width * s->height > INT32_MAX)
         return rt_fail(RT_ERR_LIMIT, "rt_render: frames above 2^31 pixels are not supported");
     const int64_t rows = rt_shard_rows_impl(s->height, rank, world, rb, nullptr);
@@ -940,7 +948,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             w.n = g.n_pixels;
             w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity)
             int *order = nullptr;
-            if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER)) {
+            if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
                 rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
                 if (rc) return rc;
                 ordered = true;

@@ -32,13 +32,15 @@ def _sums(scene, spp, **kw):
     return out.reshape(-1, 3), st
 
 
-@pytest.mark.parametrize("kernel,natural", [(0, False), (0, True), (4, False)])
+@pytest.mark.parametrize("kernel,order", [(0, "heavy"), (0, "natural"), (0, "auto"), (4, "auto")])
 @pytest.mark.parametrize("name,w,h,s", CASES)
-def test_sums_match_reference(gpu, name, w, h, s, kernel, natural):
-    """Both schedules (lane-resident with its in-frame heaviest-first order or in row-major
-    order; wavefront) against the reference's sums and traversal counters."""
+def test_sums_match_reference(gpu, name, w, h, s, kernel, order):
+    """Both schedules (lane-resident with its in-frame heaviest-first order, in row-major
+    order, or as the spp threshold picks; wavefront) against the reference's sums and
+    traversal counters."""
     scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
-    out, st = _sums(scene, s, count=True, kernel=kernel, natural_order=natural)
+    out, st = _sums(scene, s, count=True, kernel=kernel, natural_order=order == "natural",
+                    heavy_order=order == "heavy")
     g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
     ref = g["sums"].reshape(-1, 3)
     bad = (rtref.bits(out) != rtref.bits(ref)).any(1)
@@ -69,7 +71,7 @@ def test_runahead_matches_reference(gpu, name, w, h, s):
     same frame with the runahead off."""
     scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
     ref = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["sums"].reshape(h, w, 3)
-    full, _ = scene.render_sums(s)
+    full, _ = scene.render_sums(s, heavy_order=True)
     assert np.array_equal(rtref.bits(full), rtref.bits(ref))
     off, _ = scene.render_sums(s, runahead=False)
     assert np.array_equal(rtref.bits(off), rtref.bits(ref))
@@ -77,7 +79,7 @@ def test_runahead_matches_reference(gpu, name, w, h, s):
     for rank in range(8):
         rows = gpu.shard_rows(h, rank, 8, 8)
         if len(rows):
-            frame[rows] = scene.render_sums(s, rank=rank, world=8)[0]
+            frame[rows] = scene.render_sums(s, rank=rank, world=8, heavy_order=rank % 2 == 0)[0]
     assert np.array_equal(rtref.bits(frame), rtref.bits(ref))
 
 
@@ -206,21 +208,24 @@ def test_sponza_full_frame_pixels_vs_oracle(gpu, oracle):
 
 
 def test_pixel_order_does_not_change_the_frame(gpu):
-    """The default render orders pixels heaviest-first from an in-frame counting pre-pass
-    (rt_device.hip launch_order); row-major order (RT_FLAG_NATURAL_ORDER) gives the same
-    bits and counters, at several shard sizes (fewer and more pixels than lanes)."""
+    """The heaviest-first order from an in-frame counting pre-pass (rt_device.hip
+    launch_order; the default from 128 spp, RT_FLAG_HEAVY_ORDER below) and row-major order
+    (RT_FLAG_NATURAL_ORDER) give the same bits and counters, at several shard sizes (fewer
+    and more pixels than lanes)."""
     name, w, h, s = "sponza_mini", 64, 36, 4
     scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
     g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
-    a, sa = _sums(scene, s, count=True)
+    a, sa = _sums(scene, s, count=True, heavy_order=True)
     b, sb = _sums(scene, s, count=True, natural_order=True)
     assert np.array_equal(rtref.bits(a), rtref.bits(g["sums"].reshape(-1, 3)))
     assert np.array_equal(rtref.bits(a), rtref.bits(b))
     assert sa["rays"] == sb["rays"] == int(g["counters"][0])
     big = gpu.Scene.load(rtref.scene_path("sponza_mini"), 640, 360, 2)
-    x, _ = big.render_sums(2)
+    x, _ = big.render_sums(2, heavy_order=True)
     y, _ = big.render_sums(2, natural_order=True)
     assert np.array_equal(rtref.bits(x), rtref.bits(y))
+    with pytest.raises(gpu.RtError):   # the two order flags exclude each other
+        big.render_sums(2, heavy_order=True, natural_order=True)
 
 
 def test_render_multi_matches_single_device(gpu):
