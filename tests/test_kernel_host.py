@@ -264,6 +264,35 @@ def test_runahead_state_prediction(rt, kh, name, w, h):
     assert stats[2] > 0
 
 
+@pytest.mark.parametrize("per_wave", [7, 24, 64])
+def test_runahead_with_spare_lanes(rt, kh, per_wave):
+    """The runahead's management pass when a wave has idle lanes from its first iteration
+    (the harness's static allotment of `per_wave` pixels per wave, no queue: DESIGN.md §7
+    study): same bits as the per-pixel schedule, and fewer main-loop rounds than without
+    runahead."""
+    name, w, h, s = "sponza_mini", 48, 27, 6
+    v, keep = rt.make_view(rtref.ref_arrays(rt, name, w, h, s))
+    want = np.zeros((h * w, 3), np.float32)
+    kh.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
+    kh.kh_render_mega_spec.argtypes = kh.kh_render_mega.argtypes
+    kh.kh_render_mega_spec.restype = ctypes.c_int
+    kh.kh_set_static_per_wave.argtypes = [ctypes.c_int]
+    kh.kh_rounds.restype = ctypes.c_uint64
+    waves = (w * h + per_wave - 1) // per_wave
+    rounds = []
+    try:
+        kh.kh_set_static_per_wave(per_wave)
+        for fn in (kh.kh_render_mega, kh.kh_render_mega_spec):
+            out = np.zeros((h * w, 3), np.float32)
+            assert fn(ctypes.addressof(v), s, 0, 1, 8, waves, 48, None, out.ctypes.data,
+                      np.zeros(7, np.uint64).ctypes.data) == 0
+            assert np.array_equal(rtref.bits(out), rtref.bits(want))
+            rounds.append(kh.kh_rounds())
+    finally:
+        kh.kh_set_static_per_wave(0)
+    assert rounds[1] < rounds[0]
+
+
 def test_lane_resident_translucent_materials(rt, kh):
     """Materials with alpha != 1 (the reference multiplies the bounce by material.alpha,
     scene.cpp:151; every fixture is opaque): the lane-resident kernel stores alpha only for
