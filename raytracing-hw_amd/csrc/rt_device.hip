@@ -51,6 +51,14 @@ constexpr int kMegaWpeSpec = 4;
 #ifndef RT_SHADE_MIN
 #define RT_SHADE_MIN 48
 #endif
+// The runahead kernel (8-way shards, about one pixel per lane) shades at 32 READY lanes: its
+// waves thin out early, and a heavy chain's lane waits less for its batch.  8-way slowest
+// shard 294 ms at 32 (three runs 293.6-294.7) against 297-299 at 48; 28 293, 36 297, 24 298,
+// 56 307 (profiles/r02_tail_ab.jsonl).
+#ifndef RT_SPEC_SHADE_MIN
+#define RT_SPEC_SHADE_MIN 32
+#endif
+constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
@@ -300,7 +308,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         }
         const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
-        const bool shade_now = nr > 0 && (nr >= kShadeMin || nt == 0);
+        const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0);
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
