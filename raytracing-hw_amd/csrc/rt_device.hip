@@ -309,6 +309,15 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
         const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0);
+        // Runahead kernel (the 8-way shards): a traversal iteration issues at priority 1, a
+        // shading pass at 0, so waves in their long shading code give issue slots to waves
+        // stepping the frame's sample chains: slowest 8-way shard 295 -> 280 ms.  The plain
+        // kernel stays at 0 (1 GPU: 1360 -> 1395 ms with the same toggle; 4-way unchanged)
+        // (profiles/r02_tail_ab.jsonl).
+        if constexpr (kSpec) {
+            if (shade_now) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(1);
+        }
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
