@@ -1,10 +1,10 @@
 #!/bin/bash
 # A/B of LLVM scheduler strategies (make variant VFLAGS='-mllvm -amdgpu-sched-strategy=S'):
-# 1-GPU bench (frame digest must not change) and every shard of the 8-way split.
+# 1-GPU bench (frame digest must not change) and every shard of the 8-way split.  AB_LIBS="default var/x/librt_hw_amd.so ..."
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/sched_ab.jsonl
-for lib in default raytracing-hw_amd/var/ilp/librt_hw_amd.so raytracing-hw_amd/var/mc/librt_hw_amd.so raytracing-hw_amd/var/iilp/librt_hw_amd.so; do
+for lib in ${AB_LIBS:-default}; do
   if [ "$lib" = default ]; then unset RT_LIB; else export RT_LIB=$PWD/$lib; fi
   b=$(timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --fast-steps 0 --traffic-from none 2>>gpurun_out/sched_ab.err) || exit 1
   w=$(timeout -k 10 200 python -u tools/runahead_ab.py --off 0 --steps 1 --worlds 8 --full 0 2>>gpurun_out/sched_ab.err) || exit 1
