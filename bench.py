@@ -115,6 +115,66 @@ def cpu_baseline(scene_path, width, height, spp, rows, stride, threads):
             "sample": sample + " (oracle/rt_oracle.cpp restatement)", "seconds": secs}
 
 
+def pmc_mean(path, counter, kernel_prefix, duration=False):
+    """Mean per dispatch of `counter` for the parity launch of `kernel_prefix` in a rocprofv3
+    --stats PMC summary (None when absent); with duration=True, that pass's average dispatch
+    duration in seconds instead.  The fast-mode instantiation ends its template list in
+    "true>" and is skipped."""
+    import csv
+    if not os.path.exists(path):
+        return None
+    for row in csv.reader(open(path)):
+        if row and row[0].startswith(kernel_prefix) and "true>(" not in row[0] and row[1] == counter:
+            return float(row[5]) * 1e-9 if duration else float(row[4])
+    return None
+
+
+SIMDS = 256 * 4            # MI355X: 256 CUs x 4 SIMD-32
+NOMINAL_CLOCK_HZ = 2.4e9   # used only when no GRBM_GUI_ACTIVE pass is committed
+
+
+def pmc_issue(prefix, kernel_prefix):
+    """Issue-side picture of the launch from the committed SQ passes (tools/profile.sh):
+    VALU wave-instructions per SIMD per cycle over the pass's own dispatch duration (a SIMD-32
+    issues a wave64 VALU instruction in 2 cycles, so 0.5 is its ceiling), the VALU lane
+    utilisation and the wait share."""
+    sq1, sq2 = prefix + "_sq1_1080p256.csv", prefix + "_sq2_1080p256.csv"
+    valu = pmc_mean(sq2, "SQ_INSTS_VALU", kernel_prefix)
+    salu = pmc_mean(sq2, "SQ_INSTS_SALU", kernel_prefix)
+    tcv = pmc_mean(sq1, "SQ_THREAD_CYCLES_VALU", kernel_prefix)
+    aiv = pmc_mean(sq1, "SQ_ACTIVE_INST_VALU", kernel_prefix)
+    wait = pmc_mean(sq1, "SQ_WAIT_ANY", kernel_prefix)
+    wcyc = pmc_mean(sq1, "SQ_WAVE_CYCLES", kernel_prefix)
+    grbm = pmc_mean(sq1, "GRBM_GUI_ACTIVE", kernel_prefix)
+    avg_s = pmc_mean(sq2, "SQ_INSTS_VALU", kernel_prefix, duration=True)
+    if valu is None or not avg_s:
+        return None
+    clock = grbm / 8.0 / avg_s if grbm else NOMINAL_CLOCK_HZ
+    per_simd_cycle = valu / (SIMDS * avg_s * clock)
+    return {"valu_inst_per_simd_cycle": round(per_simd_cycle, 4),
+            "issue_frac": round(per_simd_cycle / 1.0, 4),
+            "issue_frac_of_simd32_peak": round(per_simd_cycle / 0.5, 4),
+            "lane_util": None if not (tcv and aiv) else round(tcv / (aiv * 64.0), 4),
+            "salu_per_valu": None if salu is None else round(salu / valu, 4),
+            "wait_any_frac": None if not (wait and wcyc) else round(wait / wcyc, 4),
+            "clock_hz": round(clock / 1e6, 1) * 1e6,
+            "clock_source": "GRBM_GUI_ACTIVE / 8 / launch time" if grbm else "nominal 2.4 GHz (no GRBM pass)",
+            "source": os.path.relpath(sq2, ROOT) + " + " + os.path.relpath(sq1, ROOT)}
+
+
+def reference_frame_sha1(scene, W, H, S):
+    """sha1 of the reference's own finished 8-bit frame of this workload, if one is committed
+    (tests/golden/golden_meta.json "frames", tools/make_goldens.py --frames)."""
+    try:
+        meta = json.load(open(os.path.join(ROOT, "tests", "golden", "golden_meta.json")))
+    except Exception:  # noqa: BLE001
+        return None
+    for f in meta.get("frames", {}).values():
+        if (f["scene"], f["width"], f["height"], f["spp"]) == (scene, W, H, S):
+            return f["frame_u8_sha1"]
+    return None
+
+
 def pmc_traffic(fetch_csv, write_csv, kernel_prefix):
     """HBM-side bytes per launch of `kernel_prefix` from rocprofv3 PMC summaries
     (tools/profile.sh, separate --pmc passes of the same command): FETCH_SIZE doubled (the
@@ -323,7 +383,7 @@ def main():
             bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
             kname = "rt_mega_kernel"
         achieved = bytes_launch / avg_s / 1e9
-        traffic, traffic_u, traffic_src = None, None, None
+        traffic, traffic_u, traffic_src, issue = None, None, None, None
         if args.traffic_from != "none":
             prefix = args.traffic_from
             default_cfg = (args.scene, W, H, S, args.kernel, world) == ("sponza", 1920, 1080, 256, 0, 1)
@@ -336,6 +396,14 @@ def main():
                     if t is not None:
                         traffic, traffic_u = t[0] / launches, t[1] / launches
                         traffic_src = os.path.relpath(fc, ROOT) + " + " + os.path.relpath(wc, ROOT)
+                issue = pmc_issue(prefix, "void " + kname + "<false")
+        frac = achieved / HBM_PEAK_GBS
+        traffic_frac = None if traffic is None else traffic / avg_s / 1e9 / HBM_PEAK_GBS
+        # the label follows the counters: HBM-bound only when the measured HBM-side traffic is
+        # at least half of what the algorithmic model asks for
+        bound = ("hbm (algorithmic model only: no PMC pass)" if traffic_frac is None
+                 else "hbm" if traffic_frac >= 0.5 * frac else "latency/issue")
+        ref_sha = reference_frame_sha1(args.scene, W, H, S)
         line = {
             "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -361,12 +429,16 @@ def main():
                        "order_ms": round(float(np.mean(order_ms)), 3),
                        "rays_per_frame": int(rays_per_frame), "samples_per_frame": W * H * S,
                        "msamples_per_s": round(W * H * S * args.steps / elapsed / 1e6, 3),
-                       "scene_load_s": round(load_s, 3), "frame_sha1": digest},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                       "scene_load_s": round(load_s, 3), "frame_sha1": digest,
+                       "reference_frame_sha1": None if ref_sha is None else ref_sha[:16],
+                       "frame_matches_reference": None if ref_sha is None else digest == ref_sha[:16]},
+            "roofline": {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(frac, 4),
                          "traffic": None if traffic is None else int(traffic),
                          "traffic_undoubled": None if traffic_u is None else int(traffic_u),
-                         "traffic_frac": None if traffic is None else round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic_frac": None if traffic_frac is None else round(traffic_frac, 4),
+                         "issue": issue,
+                         "issue_frac": None if issue is None else issue["issue_frac"],
                          "traffic_source": traffic_src,
                          "kernel": kname, "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
                          "launches_per_frame": launches,
@@ -381,10 +453,15 @@ def main():
             "fast_mode": fast_line,
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or os.cpu_count() or 1
+            # the host cores this process may use: min(nproc, cgroup quota); --cpu-threads overrides
+            quota = cpu_quota()
+            usable = os.cpu_count() or 1
+            if quota:
+                usable = max(1, min(usable, int(quota)))
+            threads = args.cpu_threads or usable
             cb = cpu_baseline(path, W, H, args.cpu_spp, min(args.cpu_rows, H), args.cpu_stride, threads)
             cb["nproc"] = os.cpu_count()
-            cb["cgroup_cpu_quota"] = cpu_quota()
+            cb["cgroup_cpu_quota"] = quota
             line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
     if world > 1:

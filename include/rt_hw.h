@@ -9,8 +9,10 @@
  *   rt_render / rt_render_device
  *                        <- Scene::render sample loop   src/core/scene.cpp:17-52
  *                           (per-pixel float RGB sums = sample_canvas, scene.cpp:20,42)
- *   rt_render_multi      <- the same loop over every GPU of the node (one row-block shard
- *                           per device, frame assembled on the host)
+ *   rt_render_frame      <- the same loop over every GPU of the node (one row-block shard
+ *                           per device), finished to 8 bits on each device and gathered
+ *                           device-to-device onto one GPU (scene.cpp:17-64, canvas.h:76-89)
+ *   rt_render_multi      <- the float frame of the same split (ABI 3 entry)
  *   rt_tonemap_u8        <- Scene::render frame finish  src/core/scene.cpp:54-64
  *   rt_tonemap_u8_device <- the same finish on the GPU   src/core/scene.cpp:54-64
  *   rt_write_ppm         <- Canvas::write_to            src/render/canvas.h:76-89
@@ -33,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum rt_status {
     RT_OK = 0,
@@ -139,13 +141,14 @@ typedef struct {
     uint64_t light_tri_tests;
     uint64_t shading_hits;  /* scene hits that were shaded (texture / attribute fetches)  */
     double render_ms;       /* device time of the whole render (order pre-pass included), HIP events;
-                               rt_render_multi: the slowest device                           */
+                               rt_render_frame / _multi: the slowest device (its shards summed) */
     /* RT_FLAG_KERNEL_TIMES (wavefront path): summed launch durations and launch counts   */
     double extend_ms, shade_ms;
     uint64_t extend_launches, shade_launches;
     uint64_t extend_rays;   /* rays traced by the extend launches (always filled)          */
     double order_ms;        /* part of render_ms spent building the pixel order            */
-    double gather_ms;       /* rt_render_multi: host assembly of the frame (slowest device) */
+    double gather_ms;       /* rt_render_frame / _multi: device-to-device copies of the slowest
+                               device + assembly on the root device + the copy to the host  */
     uint64_t devices;       /* devices that rendered                                       */
 } rt_stats;
 
@@ -176,6 +179,16 @@ int rt_render_device(rt_scene *scene, const rt_params *params, float *d_out_sum,
  * params->row_block); params->rank / world / device are ignored.  out_sum: W*H*3 floats,
  * host memory, row-major.  Bits do not depend on n_devices. */
 int rt_render_multi(rt_scene *scene, const rt_params *params, int32_t n_devices, float *out_sum, rt_stats *stats);
+/* The whole frame as shards 0 .. n_shards-1 of a (world = n_shards, params->row_block) split,
+ * shard r rendered on device devices[r] (devices NULL: device r; a device given several shards
+ * renders them one after another).  Each shard is rendered and finished to 8 bits on its own
+ * device (scene.cpp:54-64), then copied device-to-device (hipMemcpyPeerAsync, xGMI between
+ * MI355X) to devices[0], which places the rows in frame order; the frame leaves the devices
+ * in one copy per output.  out_rgb: W*H*3 bytes, the reference's canvas (canvas.h:76-89);
+ * out_sum: W*H*3 floats (sample_canvas, scene.cpp:20,42); either may be NULL, not both.
+ * params->rank / world / device are ignored.  Bits do not depend on n_shards or devices. */
+int rt_render_frame(rt_scene *scene, const rt_params *params, int32_t n_shards, const int32_t *devices,
+                    uint8_t *out_rgb, float *out_sum, rt_stats *stats);
 
 /* Closest hit + light pdf for n explicit rays (BVH::intersect bvh.cpp:239-243 and
  * ManyLightsDistribution::pdf random.cpp:179-188; origin/dir as given to Ray::Ray, which

@@ -8,9 +8,11 @@
 //      objects, bvh.nodes, the light list + its BVH as ManyLightsDistribution builds them
 //      (random.cpp:156-168), materials, textures and the camera (camera.h:22-30);
 //   2. hands them to rt_scene_from_view and renders the frame on every GPU of the node with
-//      rt_render_multi (row-block shards, one host thread per device);
-//   3. finishes the float sums exactly as Scene::render does (rt_tonemap_u8) and writes them
-//      into scene.camera->canvas, so scene.draw_into(output) (canvas.h:76-89) is unchanged.
+//      rt_render_frame (row-block shards, one host thread per device; each shard finished to
+//      8 bits on its GPU exactly as Scene::render finishes it, scene.cpp:54-64, and gathered
+//      device-to-device onto GPU 0);
+//   3. writes the 8-bit frame into scene.camera->canvas, so scene.draw_into(output)
+//      (canvas.h:76-89) is unchanged.
 // Errors come back as status codes and are rethrown as std::runtime_error, the reference's
 // convention.  Built against the reference's unmodified headers and objects by
 // oracle/Makefile (`make -C oracle integration` -> oracle/_ref/render_mi355x).
@@ -182,15 +184,14 @@ void render_on_mi355x(Scene &s, int n_gpus, rt_stats *st) {
     rt_scene *rs = nullptr;
     check(rt_scene_from_view(&f.view, &rs));
     const int W = f.view.width, H = f.view.height;
-    std::vector<float> sum((size_t)W * H * 3);
     rt_params p{};
     p.spp = s.samples;
     p.row_block = 8;
-    int rc = rt_render_multi(rs, &p, n_gpus, sum.data(), st);
+    // the finished 8-bit frame, gathered device-to-device onto GPU 0 (rt_render_frame)
+    std::vector<uint8_t> rgb((size_t)W * H * 3);
+    int rc = rt_render_frame(rs, &p, n_gpus, nullptr, rgb.data(), nullptr, st);
     rt_scene_free(rs);
     check(rc);
-    std::vector<uint8_t> rgb(sum.size());
-    check(rt_tonemap_u8(sum.data(), W, H, s.samples, rgb.data()));
     for (int j = 0; j < H; ++j)
         for (int i = 0; i < W; ++i) {
             const uint8_t *c = &rgb[3 * ((size_t)j * W + i)];

@@ -44,7 +44,7 @@ class RtSceneView(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 3          # include/rt_hw.h RT_ABI_VERSION
+ABI_VERSION = 4          # include/rt_hw.h RT_ABI_VERSION
 KERNEL_LANE = 0          # RT_KERNEL_LANE: lane-resident persistent kernel (default)
 KERNEL_WAVEFRONT = 4     # RT_KERNEL_WAVEFRONT: init / extend / shade launches
 FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES
@@ -86,6 +86,8 @@ ABI = {
     "rt_render_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RtParams), ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.POINTER(RtStats)]),
     "rt_render_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RtParams), ctypes.c_int32, _c_f,
+                                       ctypes.POINTER(RtStats)]),
+    "rt_render_frame": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(RtParams), ctypes.c_int32, _c_i, _c_b, _c_f,
                                        ctypes.POINTER(RtStats)]),
     "rt_intersect_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_f, _c_f, _c_f,
                                          ctypes.POINTER(ctypes.c_int64)]),
@@ -244,6 +246,28 @@ class Scene:
         p = self._params(spp, 0, 1, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk)
         _check(lib().rt_render_multi(self._h, ctypes.byref(p), n_devices, out.ctypes.data_as(_c_f), ctypes.byref(st)))
         return out, st.as_dict()
+
+    def render_frame(self, spp=None, n_shards=0, devices=None, row_block=8, sums=True, rgb=True, kernel=0,
+                     fast=False, fast_chunk=0, runahead=True):
+        """The whole frame as shards 0..n_shards-1 (0 = one per visible device), shard r on
+        device devices[r] (None: device r; rt_render_frame): each shard is finished to 8 bits
+        on its device and gathered device-to-device onto devices[0].  Returns (rgb (H, W, 3)
+        uint8 or None, sums (H, W, 3) float32 or None, stats)."""
+        out_rgb = np.zeros((self.height, self.width, 3), np.uint8) if rgb else None
+        out_sum = np.zeros((self.height, self.width, 3), np.float32) if sums else None
+        dev = None
+        if devices is not None:
+            dev = np.ascontiguousarray(devices, np.int32)
+            if n_shards and len(dev) != n_shards:
+                raise ValueError("devices must name one device per shard")
+            n_shards = len(dev)
+        st = RtStats()
+        p = self._params(spp, 0, 1, row_block, False, kernel, fast=fast, fast_chunk=fast_chunk, runahead=runahead)
+        _check(lib().rt_render_frame(self._h, ctypes.byref(p), n_shards,
+                                     dev.ctypes.data_as(_c_i) if dev is not None else None,
+                                     out_rgb.ctypes.data_as(_c_b) if rgb else None,
+                                     out_sum.ctypes.data_as(_c_f) if sums else None, ctypes.byref(st)))
+        return out_rgb, out_sum, st.as_dict()
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
                       kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0, device=0,

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -59,7 +60,14 @@ constexpr int kMegaWpeSpec = 4;
 #define RT_SPEC_SHADE_MIN 32
 #endif
 constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
-constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
+constexpr int kShadeMin = RT_SHADE_MIN;
+// Traversal iterations between two shading passes run as an inner loop of their own (no pixel
+// claim, runahead pass or schedule decision per iteration).  0: one iteration per pass of the
+// main loop (round 2), for A/B builds.
+#ifndef RT_INNER_TRAV
+#define RT_INNER_TRAV 1
+#endif
+constexpr bool kInnerTrav = RT_INNER_TRAV != 0;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -327,8 +335,26 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             pf[shade_now ? 5 : 6] += (unsigned long long)(shade_now ? nr : nt);
         }
 #endif
-        rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
-                                                                           root, S, nodes, cnt, kSpec && tail);
+        if (kInnerTrav && !LSPLIT && !shade_now) {
+            // Traversal iterations until the wave would shade (the condition above): nothing
+            // but trav_step and two ballots per iteration.  In a traversal iteration no lane
+            // ends a path, so no lane claims a pixel and a tail wave's runahead records do not
+            // change: the outer loop's work between two shading passes is only this.
+            int kt = nt;
+            do {
+                if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) L.state = rtd::M_READY;
+                const unsigned long long rb = __ballot(L.state == rtd::M_READY), tb = __ballot(L.state == rtd::M_TRAV);
+                kt = __popcll(tb);
+                if (kt == 0 || __popcll(rb) >= (kSpec ? kSpecShadeMin : kShadeMin)) break;
+#ifdef RT_MEGA_PROF
+                pf[4] += 1;
+                pf[6] += (unsigned long long)kt;
+#endif
+            } while (true);
+        } else {
+            rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
+                                                                               root, S, nodes, cnt, kSpec && tail);
+        }
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
@@ -1110,6 +1136,46 @@ void rt_device_scene_release(rt_scene *s) {
     s->blob = nullptr;
 }
 
+// Frame assembly on the root device of rt_render_frame (below).
+__global__ void __launch_bounds__(256) rt_rows_scatter_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                              const int *__restrict__ frame_row_of, long long rows,
+                                                              long long row_bytes) {
+    // rows of whole 4-byte words (row_bytes % 4 == 0: W*3 floats, or W*3 bytes with W % 4 == 0)
+    // go word by word; other widths byte by byte
+    const long long r = blockIdx.y;
+    if (r >= rows) return;
+    const uint8_t *s = src + r * row_bytes;
+    uint8_t *d = dst + (long long)frame_row_of[r] * row_bytes;
+    if ((row_bytes & 3) == 0) {
+        for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < row_bytes / 4; k += (long long)gridDim.x * blockDim.x)
+            ((uint32_t *)d)[k] = ((const uint32_t *)s)[k];
+    } else {
+        for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < row_bytes; k += (long long)gridDim.x * blockDim.x)
+            d[k] = s[k];
+    }
+}
+
+namespace {
+
+// Device buffers released on every return path (on their own device).
+struct DevBuf {
+    int dev = -1;
+    void *p = nullptr;
+    hipError_t alloc(int device, size_t bytes) {
+        dev = device;
+        DeviceGuard g(device);
+        return hipMalloc(&p, bytes ? bytes : 4);
+    }
+    ~DevBuf() {
+        if (p) {
+            DeviceGuard g(dev);
+            (void)hipFree(p);
+        }
+    }
+};
+
+}  // namespace
+
 extern "C" {
 
 int rt_scene_upload(rt_scene *s, int32_t device) {
@@ -1124,13 +1190,19 @@ int rt_render_device(rt_scene *s, const rt_params *p, float *d_out, void *stream
 int rt_tonemap_u8_device(const float *d_sum, int32_t width, int32_t height, int32_t spp, uint8_t *d_rgb, void *stream) {
     if (!d_sum || !d_rgb || width <= 0 || height <= 0 || spp <= 0)
         return rt_fail(RT_ERR_ARG, "rt_tonemap_u8_device: bad argument");
+    // the quantizer thresholds go to each device's constant memory once; threads finishing
+    // on the same device at first use serialise on the mutex
+    static std::mutex upload_mu;
     static bool uploaded[kRtMaxDevices] = {false};
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     if (dev < 0 || dev >= kRtMaxDevices) return rt_fail(RT_ERR_DEVICE, "rt_tonemap_u8_device: device id");
-    if (!uploaded[dev]) {
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(k_quant_thr), rtm::kQuantThr, sizeof rtm::kQuantThr));
-        uploaded[dev] = true;
+    {
+        std::lock_guard<std::mutex> lock(upload_mu);
+        if (!uploaded[dev]) {
+            HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(k_quant_thr), rtm::kQuantThr, sizeof rtm::kQuantThr));
+            uploaded[dev] = true;
+        }
     }
     const long long n = (long long)width * height * 3;
     const unsigned blocks = (unsigned)std::min<long long>((n + 255) / 256, 4096);
@@ -1145,10 +1217,167 @@ int rt_render(rt_scene *s, const rt_params *p, float *out, rt_stats *st) {
     return render_host(s, p, out, st);
 }
 
-// The whole frame over devices 0 .. n-1 (n <= 0: every visible device): one host thread per
-// device renders the row-block shard rank = device of world = n (params' rank and world are
-// ignored) on that device's copy of the scene, copies it to the host and writes its rows
-// into the frame.  Shards own disjoint rows, so the threads write disjoint parts of out.
+// The whole frame as shards 0 .. n-1 of a (world n, row_block) split, shard r on device
+// devices[r] (include/rt_hw.h rt_render_frame).  One host thread per distinct device renders
+// that device's shards one after another (one render per (scene, device) in flight), finishes
+// each to 8 bits on the same device (rt_finish_kernel, scene.cpp:54-64) and copies it, 8-bit
+// frame and (if asked) float sums, device-to-device into a staging buffer on the root device
+// devices[0] (hipMemcpyPeerAsync: over xGMI between MI355X).  The root then places the rows
+// in frame order (rt_rows_scatter_kernel; the reference's canvas, canvas.h:76-89, is row-major)
+// and the frame leaves the devices in one copy per output.
+int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int32_t *devices, uint8_t *out_rgb,
+                    float *out_sum, rt_stats *st) {
+    if (!s || !p || (!out_rgb && !out_sum)) return rt_fail(RT_ERR_ARG, "rt_render_frame: NULL argument");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    const int n = n_shards > 0 ? n_shards : ndev;
+    if (n < 1 || n > (1 << 16)) return rt_fail(RT_ERR_ARG, "rt_render_frame: bad shard count " + std::to_string(n));
+    std::vector<int> dev_of(n);
+    for (int r = 0; r < n; ++r) {
+        dev_of[r] = devices ? devices[r] : r;
+        if (dev_of[r] < 0 || dev_of[r] >= ndev || dev_of[r] >= kRtMaxDevices)
+            return rt_fail(RT_ERR_DEVICE, "rt_render_frame: shard " + std::to_string(r) + " on device " +
+                                              std::to_string(dev_of[r]) + ", " + std::to_string(ndev) + " visible");
+    }
+    const int spp = p->spp > 0 ? p->spp : s->samples;
+    if (spp < 1) return rt_fail(RT_ERR_ARG, "rt_render_frame: samples per pixel must be >= 1");
+    int rc = ensure_blob(s);   // built once here, copied to every device
+    if (rc) return rc;
+    const int rb = p->row_block > 0 ? p->row_block : 8, W = s->width, H = s->height;
+    const int root = dev_of[0];
+    // staging on the root: shard r's rows at row offset base[r]; frame_row_of[staging row]
+    std::vector<int64_t> rows(n), base(n + 1, 0);
+    std::vector<int32_t> frame_row_of((size_t)std::max(H, 1));
+    for (int r = 0; r < n; ++r) {
+        rows[r] = rt_shard_rows_impl(H, r, n, rb, nullptr);
+        if (rows[r] < 0) return RT_ERR_ARG;
+        rt_shard_rows_impl(H, r, n, rb, frame_row_of.data() + base[r]);
+        base[r + 1] = base[r] + rows[r];
+    }
+    const size_t row_u8 = (size_t)W * 3, row_f = row_u8 * sizeof(float);
+    DevBuf stage_u8, stage_f, frame_u8, frame_f, row_map;
+    HIP_TRY(stage_u8.alloc(root, (size_t)H * row_u8));
+    HIP_TRY(frame_u8.alloc(root, (size_t)H * row_u8));
+    if (out_sum) {
+        HIP_TRY(stage_f.alloc(root, (size_t)H * row_f));
+        HIP_TRY(frame_f.alloc(root, (size_t)H * row_f));
+    }
+    HIP_TRY(row_map.alloc(root, (size_t)std::max(H, 1) * sizeof(int32_t)));
+    {
+        DeviceGuard g(root);
+        HIP_TRY(hipMemcpy(row_map.p, frame_row_of.data(), (size_t)H * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    std::vector<int> uniq;
+    for (int d : dev_of)
+        if (std::find(uniq.begin(), uniq.end(), d) == uniq.end()) uniq.push_back(d);
+    for (int d : uniq) {   // direct xGMI copies between the root and its peers where the runtime allows
+        if (d == root) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, d, root) == hipSuccess && can) {
+            DeviceGuard g(d);
+            (void)hipDeviceEnablePeerAccess(root, 0);
+            (void)hipGetLastError();   // (already enabled is not an error here)
+        }
+        if (hipDeviceCanAccessPeer(&can, root, d) == hipSuccess && can) {
+            DeviceGuard g(root);
+            (void)hipDeviceEnablePeerAccess(d, 0);
+            (void)hipGetLastError();
+        }
+    }
+    std::vector<int> rcs(uniq.size(), RT_OK);
+    std::vector<std::string> errs(uniq.size());
+    std::vector<rt_stats> sts(n);
+    std::vector<double> copy_ms(uniq.size(), 0.0);
+    auto work = [&](size_t ui) {
+        const int dev = uniq[ui];
+        auto fail = [&](int code, const std::string &m) {
+            rcs[ui] = rt_fail(code, m);
+            errs[ui] = rt_last_error();
+        };
+        int r0 = ensure_device_scene(s, dev);
+        if (r0) { rcs[ui] = r0; errs[ui] = rt_last_error(); return; }
+        DeviceGuard g(dev);
+        if (!g.ok) return fail(RT_ERR_DEVICE, "hipSetDevice failed");
+        hipStream_t stream = nullptr;
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+            return fail(RT_ERR_DEVICE, "hipStreamCreate failed");
+        int64_t max_rows = 0;
+        for (int r = 0; r < n; ++r)
+            if (dev_of[r] == dev) max_rows = std::max(max_rows, rows[r]);
+        DevBuf sum, rgb;
+        hipError_t e = sum.alloc(dev, (size_t)max_rows * row_f);
+        if (e == hipSuccess) e = rgb.alloc(dev, (size_t)max_rows * row_u8);
+        for (int r = 0; r < n && e == hipSuccess && rcs[ui] == RT_OK; ++r) {
+            if (dev_of[r] != dev || rows[r] == 0) continue;
+            rt_params q = *p;
+            q.rank = r;
+            q.world = n;
+            q.row_block = rb;
+            q.device = dev;
+            q.spp = spp;
+            int lr = launch(s, &q, (float *)sum.p, stream, &sts[r]);   // waits (stats)
+            if (lr) { rcs[ui] = lr; errs[ui] = rt_last_error(); break; }
+            lr = rt_tonemap_u8_device((const float *)sum.p, W, (int32_t)rows[r], spp, (uint8_t *)rgb.p, stream);
+            if (lr) { rcs[ui] = lr; errs[ui] = rt_last_error(); break; }
+            const auto t0 = std::chrono::steady_clock::now();
+            e = hipMemcpyPeerAsync((uint8_t *)stage_u8.p + base[r] * row_u8, root, rgb.p, dev, rows[r] * row_u8, stream);
+            if (e == hipSuccess && out_sum)
+                e = hipMemcpyPeerAsync((uint8_t *)stage_f.p + base[r] * row_f, root, sum.p, dev, rows[r] * row_f, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            copy_ms[ui] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        if (e != hipSuccess && rcs[ui] == RT_OK) fail(RT_ERR_DEVICE, std::string("rt_render_frame: ") + hipGetErrorString(e));
+        (void)hipStreamDestroy(stream);
+    };
+    std::vector<std::thread> threads;
+    for (size_t ui = 1; ui < uniq.size(); ++ui) threads.emplace_back(work, ui);
+    work(0);
+    for (std::thread &t : threads) t.join();
+    for (size_t ui = 0; ui < uniq.size(); ++ui)
+        if (rcs[ui] != RT_OK) return rt_fail(rcs[ui], "device " + std::to_string(uniq[ui]) + ": " + errs[ui]);
+    // assemble on the root, one copy to the host per output
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+        DeviceGuard g(root);
+        if (!g.ok) return rt_fail(RT_ERR_DEVICE, "hipSetDevice failed");
+        if (H > 0) {
+            hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(4, (unsigned)H), dim3(256), 0, nullptr,
+                               (const uint8_t *)stage_u8.p, (uint8_t *)frame_u8.p, (const int *)row_map.p, (long long)H,
+                               (long long)row_u8);
+            HIP_TRY(hipGetLastError());
+            if (out_sum) {
+                hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(8, (unsigned)H), dim3(256), 0, nullptr,
+                                   (const uint8_t *)stage_f.p, (uint8_t *)frame_f.p, (const int *)row_map.p,
+                                   (long long)H, (long long)row_f);
+                HIP_TRY(hipGetLastError());
+            }
+        }
+        if (out_rgb) HIP_TRY(hipMemcpy(out_rgb, frame_u8.p, (size_t)H * row_u8, hipMemcpyDeviceToHost));
+        if (out_sum) HIP_TRY(hipMemcpy(out_sum, frame_f.p, (size_t)H * row_f, hipMemcpyDeviceToHost));
+    }
+    const double assemble_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        std::vector<double> dev_ms(uniq.size(), 0.0), dev_order(uniq.size(), 0.0);   // a device's shards run in turn
+        for (int r = 0; r < n; ++r) {
+            const rt_stats &x = sts[r];
+            st->pixels += x.pixels; st->samples += x.samples; st->rays += x.rays;
+            st->aabb_tests += x.aabb_tests; st->tri_tests += x.tri_tests; st->light_queries += x.light_queries;
+            st->light_aabb_tests += x.light_aabb_tests; st->light_tri_tests += x.light_tri_tests;
+            st->shading_hits += x.shading_hits; st->extend_rays += x.extend_rays;
+            const size_t ui = (size_t)(std::find(uniq.begin(), uniq.end(), dev_of[r]) - uniq.begin());
+            dev_ms[ui] += x.render_ms;
+            dev_order[ui] += x.order_ms;
+        }
+        st->render_ms = *std::max_element(dev_ms.begin(), dev_ms.end());
+        st->order_ms = *std::max_element(dev_order.begin(), dev_order.end());
+        st->gather_ms = *std::max_element(copy_ms.begin(), copy_ms.end()) + assemble_ms;
+        st->devices = (uint64_t)uniq.size();
+    }
+    return RT_OK;
+}
+
+// The float frame over devices 0 .. n-1 (ABI 3 entry; rt_render_frame with shard r on device r).
 int rt_render_multi(rt_scene *s, const rt_params *p, int32_t n_devices, float *out, rt_stats *st) {
     if (!s || !p || !out) return rt_fail(RT_ERR_ARG, "rt_render_multi: NULL argument");
     int ndev = 0;
@@ -1157,57 +1386,7 @@ int rt_render_multi(rt_scene *s, const rt_params *p, int32_t n_devices, float *o
     if (n < 1 || n > ndev || n > kRtMaxDevices)
         return rt_fail(RT_ERR_DEVICE, "rt_render_multi: " + std::to_string(n) + " devices requested, " +
                                           std::to_string(ndev) + " visible");
-    int rc = ensure_blob(s);   // built once here, copied by every thread
-    if (rc) return rc;
-    const int rb = p->row_block > 0 ? p->row_block : 8;
-    std::vector<int> rcs(n, RT_OK);
-    std::vector<std::string> errs(n);
-    std::vector<rt_stats> sts(n);
-    std::vector<double> gather_ms(n, 0.0);
-    auto work = [&](int dev) {
-        rt_params q = *p;
-        q.rank = dev;
-        q.world = n;
-        q.row_block = rb;
-        q.device = dev;
-        const int64_t rows = rt_shard_rows_impl(s->height, dev, n, rb, nullptr);
-        std::vector<int32_t> row_ids((size_t)std::max<int64_t>(rows, 1));
-        rt_shard_rows_impl(s->height, dev, n, rb, row_ids.data());
-        std::vector<float> part((size_t)std::max<int64_t>(rows, 1) * s->width * 3);
-        int r = render_host(s, &q, part.data(), &sts[dev]);
-        if (r == RT_OK) {
-            const auto t0 = std::chrono::steady_clock::now();
-            const size_t row_floats = (size_t)s->width * 3;
-            for (int64_t k = 0; k < rows; ++k)
-                std::memcpy(out + (size_t)row_ids[k] * row_floats, part.data() + (size_t)k * row_floats,
-                            row_floats * sizeof(float));
-            gather_ms[dev] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        } else {
-            errs[dev] = rt_last_error();
-        }
-        rcs[dev] = r;
-    };
-    std::vector<std::thread> threads;
-    for (int dev = 1; dev < n; ++dev) threads.emplace_back(work, dev);
-    work(0);
-    for (std::thread &t : threads) t.join();
-    for (int dev = 0; dev < n; ++dev)
-        if (rcs[dev] != RT_OK) return rt_fail(rcs[dev], "device " + std::to_string(dev) + ": " + errs[dev]);
-    if (st) {
-        std::memset(st, 0, sizeof *st);
-        for (int dev = 0; dev < n; ++dev) {
-            const rt_stats &x = sts[dev];
-            st->pixels += x.pixels; st->samples += x.samples; st->rays += x.rays;
-            st->aabb_tests += x.aabb_tests; st->tri_tests += x.tri_tests; st->light_queries += x.light_queries;
-            st->light_aabb_tests += x.light_aabb_tests; st->light_tri_tests += x.light_tri_tests;
-            st->shading_hits += x.shading_hits; st->extend_rays += x.extend_rays;
-            st->render_ms = std::max(st->render_ms, x.render_ms);
-            st->order_ms = std::max(st->order_ms, x.order_ms);
-            st->gather_ms = std::max(st->gather_ms, gather_ms[dev]);
-        }
-        st->devices = (uint64_t)n;
-    }
-    return RT_OK;
+    return rt_render_frame(s, p, n, nullptr, nullptr, out, st);
 }
 
 int rt_intersect_rays(rt_scene *s, int64_t n, const float *org, const float *dir, float *out_f, int64_t *out_i) {

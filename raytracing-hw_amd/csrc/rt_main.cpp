@@ -2,7 +2,8 @@
 //   rt_solution input.gltf width height samples [output.ppm]
 // Same positional arguments, same default output name, same terminate-with-message
 // behaviour on errors (std::runtime_error), rendering through librt_hw_amd on every GPU of
-// the node (rt_render_multi: one row-block shard per device; RT_GPUS=n uses devices 0..n-1).
+// the node (rt_render_frame: one row-block shard per device, finished on its GPU and gathered
+// device-to-device onto GPU 0; RT_GPUS=n uses devices 0..n-1).
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -40,11 +41,10 @@ int main(int argc, char *argv[]) {
     rt_params p{};
     p.spp = samples;
     p.row_block = 8;
-    std::vector<float> sum((size_t)width * height * 3);
     rt_stats st{};
-    check(rt_render_multi(scene, &p, n_gpus, sum.data(), &st));
+    // every shard finished to 8 bits on its GPU and gathered device-to-device onto GPU 0
     std::vector<uint8_t> rgb((size_t)width * height * 3);
-    check(rt_tonemap_u8(sum.data(), width, height, samples, rgb.data()));
+    check(rt_render_frame(scene, &p, n_gpus, nullptr, rgb.data(), nullptr, &st));
     double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::cout << "      " << total << " seconds (" << total * 1000 << " ms) elapsed; render " << st.render_ms
               << " ms on " << st.devices << " MI355X." << std::endl;

@@ -26,7 +26,8 @@ def declared_functions():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for must in ["rt_scene_load_gltf", "rt_scene_from_view", "rt_render", "rt_render_device", "rt_intersect_rays",
-                 "rt_tonemap_u8", "rt_write_ppm", "rt_shard_rows", "rt_last_error", "rt_abi_version"]:
+                 "rt_tonemap_u8", "rt_write_ppm", "rt_shard_rows", "rt_last_error", "rt_abi_version",
+                 "rt_render_multi", "rt_render_frame"]:
         assert must in names
 
 
@@ -38,7 +39,7 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 3
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 4
     assert ctypes.sizeof(rt.RtParams) == 36
     assert ctypes.sizeof(rt.RtStats) == 9 * 8 + 3 * 8 + 3 * 8 + 3 * 8
 
@@ -92,9 +93,11 @@ def test_errors_are_reported(rt, tmp_path):
     assert lib.rt_render(s.handle, ctypes.byref(p), None, None) == -1   # RT_ERR_ARG
     out = np.zeros(8 * 8 * 3, np.float32)
     assert lib.rt_render_multi(s.handle, ctypes.byref(p), 1, None, None) == -1   # RT_ERR_ARG
+    assert lib.rt_render_frame(s.handle, ctypes.byref(p), 1, None, None, None, None) == -1   # no output
     if rt.device_count() == 0:   # no GPU: every render entry fails loudly (no CPU fallback)
         assert lib.rt_render(s.handle, ctypes.byref(p), out.ctypes.data_as(rt._c_f), None) == -4   # RT_ERR_DEVICE
         assert lib.rt_render_multi(s.handle, ctypes.byref(p), 0, out.ctypes.data_as(rt._c_f), None) == -4
+        assert lib.rt_render_frame(s.handle, ctypes.byref(p), 2, None, None, out.ctypes.data_as(rt._c_f), None) == -4
     assert lib.rt_tonemap_u8(None, 4, 4, 1, None) == -1
 
 

@@ -1,0 +1,42 @@
+"""The whole-frame goldens of the BASELINE frames (tools/make_goldens.py --frames: the
+reference's own render of C3 and the headline, scene.cpp:31-64) are self-consistent, and the
+host frame finish (rt_tonemap_u8, scene.cpp:54-64) turns their float rows into the
+reference's 8-bit rows.  CPU only; the GPU comparison is tests/test_gpu_configs.py
+test_whole_frame_matches_reference."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import rtref
+
+FRAMES = json.load(open(os.path.join(rtref.GOLD, "golden_meta.json"))).get("frames", {})
+
+
+@pytest.mark.parametrize("config", ["c3", "headline"])
+def test_frame_golden_is_consistent(rt, config):
+    f = FRAMES[config]
+    W, H, S = f["width"], f["height"], f["spp"]
+    g = rtref.golden(f["file"])
+    assert g["row_fnv1a"].shape == (H,)
+    rows = g["rows"]
+    assert np.array_equal(rtref.row_hash(g["row_sums"]), g["row_fnv1a"][rows])
+    assert int(g["counters"][0]) == f["sums"]["rays"]
+    if "row_u8" in g:
+        assert np.array_equal(rt.tonemap(g["row_sums"], S), g["row_u8"])
+
+
+def test_bench_knows_the_reference_frame():
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(rtref.ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    argv = sys.argv
+    try:
+        spec.loader.exec_module(b)
+    finally:
+        sys.argv = argv
+    f = FRAMES["headline"]
+    assert b.reference_frame_sha1("sponza", 1920, 1080, 256) == f["frame_u8_sha1"]
+    assert b.reference_frame_sha1("sponza", 1920, 1080, 1024) is None

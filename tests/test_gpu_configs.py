@@ -5,7 +5,11 @@ sources, oracle/ref_harness `pixels`, per-pixel RNG convention of SURVEY.md §8c
   C3        sponza proxy 1024x1024x256, whole frame on one GPU
   headline  sponza proxy 1920x1080x256, whole frame on one GPU
   C4        sponza proxy 1920x1080x1024, each of the 8 row-block shards of the 8-GPU split
-  C5        dragon-100k + sponza proxy 3840x2160x4096, rank 0's shard of the 8-GPU split
+  C5        dragon-100k + sponza proxy 3840x2160x4096, rank 0's shard of the 8-GPU split, and
+            64 pixels of each of ranks 1-7 at full spp
+  whole frames: C3 and the headline, every row of the float frame (per-row FNV-1a hashes of
+            the reference's own full render, tools/make_goldens.py --frames), 8 full rows,
+            the frame counters, and the sha1 of the reference's finished 8-bit frame
 
 These are the frames whose per-pixel sample chains (256 to 4096 sequential samples, RNG
 state and pixel sum held in LDS between uses: rt_mega.h) the small parity cases cannot reach.
@@ -22,7 +26,9 @@ import pytest
 import rtref
 
 pytestmark = pytest.mark.gpu
-META = json.load(open(os.path.join(rtref.GOLD, "golden_meta.json")))["configs"]
+_META = json.load(open(os.path.join(rtref.GOLD, "golden_meta.json")))
+META = _META["configs"]
+FRAMES = _META.get("frames", {})
 SCENE_DIR = os.path.join(tempfile.gettempdir(), "rt_scenes")
 
 
@@ -113,3 +119,41 @@ def test_c5_fast_mode_full_spp(gpu, oracle):
         p = int(rows[k // W]) * W + int(k % W)
         ref, _ = oracle.render_fast(arrays, S, chunk, p, p + 1, threads=1)
         assert np.array_equal(rtref.bits(out[k // W, k % W]), rtref.bits(ref[0])), f"pixel {p}"
+
+
+def test_c5_ranks_1_to_7_match_reference(gpu):
+    """64 seeded pixels of each of ranks 1-7 of C5's 8-way split at 4096 spp (rank 0 above)."""
+    c = META["c5_ranks"]
+    W, H, S, world = c["width"], c["height"], c["spp"], c["world"]
+    scene = _scene(gpu, c["scene"], W, H, S)
+    g = rtref.golden(c["file"])
+    checked = 0
+    for rank in c["ranks"]:
+        out, _ = scene.render_sums(S, rank=rank, world=world)
+        checked += _check(out, gpu.shard_rows(H, rank, world), W, g, world, rank)
+    assert checked == len(g["index"]) == 64 * len(c["ranks"])
+
+
+@pytest.mark.parametrize("config", ["c3", "headline"])
+def test_whole_frame_matches_reference(gpu, config):
+    """The whole BASELINE frame against the reference's own render of it (scene.cpp:31-64):
+    every row's FNV-1a hash of the float sums, 8 full rows bit for bit, and the sha1 of the
+    8-bit frame finished on the device (rt_finish_kernel) against the reference's PPM body.
+    C3 also counts (rays, AABB and triangle tests, light queries against the reference's)."""
+    import hashlib
+    f = FRAMES[config]
+    W, H, S = f["width"], f["height"], f["spp"]
+    assert f["scene_sha256"] == META[f["scene"]]["scene_sha256"]
+    scene = _scene(gpu, f["scene"], W, H, S)
+    count = config == "c3"
+    out, st = scene.render_sums(S, count=count)
+    g = rtref.golden(f["file"])
+    bad = np.nonzero(rtref.row_hash(out) != g["row_fnv1a"])[0]
+    assert len(bad) == 0, f"{len(bad)} of {H} rows differ, first {bad[:8]}"
+    assert np.array_equal(rtref.bits(out[g["rows"]]), rtref.bits(g["row_sums"]))
+    if count:
+        ref = f["sums"]
+        assert (st["rays"], st["aabb_tests"], st["tri_tests"], st["light_queries"], st["light_tri_tests"]) == \
+            (ref["rays"], ref["aabb"], ref["tri"], ref["light_queries"], ref["light_tri"])
+    rgb, _, _ = scene.render_frame(S, n_shards=1, devices=[0], sums=False)
+    assert hashlib.sha1(rgb.tobytes()).hexdigest() == f["frame_u8_sha1"]

@@ -4,6 +4,8 @@ Bar: bit-exact float32 per-pixel sums (the path is integer-seeded and fully IEEE
 difference is a bug), identical AABB / triangle test counts (same traversal order), and
 identical results across kernels and pixel partitions.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -239,6 +241,27 @@ def test_render_multi_matches_single_device(gpu):
         assert np.array_equal(rtref.bits(frame), rtref.bits(ref))
         assert st["devices"] == (n or gpu.device_count())
         assert st["rays"] == int(rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["counters"][0])
+
+
+@pytest.mark.parametrize("n_shards", [1, 3, 8])
+@pytest.mark.parametrize("name,w,h,s", [("sponza_mini", 64, 36, 4), ("cornell", 33, 17, 3)])
+def test_render_frame_device_gather(gpu, n_shards, name, w, h, s):
+    """rt_render_frame with every shard on device 0 (the pool's boxes have one GPU): each shard
+    rendered and finished to 8 bits on the device, copied device-to-device into the root's
+    staging buffer and placed in frame order there.  Float frame = the reference's sums and
+    8-bit frame = the reference's finished PPM, bit for bit, at 1, 3 and 8 shards (the row
+    scatter of a 3- and an 8-way split; 33 pixels = 99-byte rows take the byte path, and
+    17 rows of 4-row blocks leave shards 5-7 empty).  The n > 1 device case (xGMI peer copies
+    between MI355X) runs the same code with other device ids; it is not exercised on one GPU."""
+    scene = gpu.Scene.load(rtref.scene_path(name), w, h, s)
+    ref = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")["sums"].reshape(h, w, 3)
+    ppm = open(os.path.join(rtref.GOLD, f"{name}_{w}x{h}x{s}.ppm"), "rb").read()
+    rgb, sums, st = scene.render_frame(s, devices=[0] * n_shards, row_block=4)
+    assert np.array_equal(rtref.bits(sums), rtref.bits(ref))
+    assert rgb.tobytes() == ppm[len(b"P6\n%d %d\n255\n" % (w, h)):]
+    assert st["devices"] == 1 and st["pixels"] == w * h and st["gather_ms"] > 0
+    rgb2, none, _ = scene.render_frame(s, devices=[0] * n_shards, row_block=4, sums=False)
+    assert none is None and np.array_equal(rgb2, rgb)
 
 
 def test_concurrent_scenes_on_one_device(gpu):

@@ -152,6 +152,52 @@ def config_goldens(meta):
         print(name, meta["configs"][name]["pixels"], flush=True)
 
 
+FRAMES = [("c3", "sponza", 1024, 1024, 256), ("headline", "sponza", 1920, 1080, 256)]
+C5_RANKS_PIXELS = 64     # pixels per rank for the every-rank C5 golden
+
+
+def frame_goldens(meta, save, threads=8):
+    """Whole BASELINE frames rendered by the reference (ref_harness sums, scene.cpp:31-64):
+    per-row FNV-1a hashes of every row's float sums, 8 full rows, the frame's counters and the
+    sha1 of the reference's finished 8-bit frame (the body of its PPM, canvas.h:76-89)."""
+    meta.setdefault("frames", {})
+    for name, scene, W, H, S in FRAMES:
+        out = os.path.join(GOLD, f"{name}_{scene}_rowhash_{W}x{H}x{S}.rtd")
+        if os.path.exists(out) and name in meta["frames"]:
+            continue
+        path = scenes.ensure_scene(scene, SCENE_DIR)
+        full, ppm = f"/tmp/{name}_{scene}_{W}x{H}x{S}.rtd", f"/tmp/{name}_{scene}_{W}x{H}x{S}.ppm"
+        info = harness("sums", path, W, H, S, full, threads, ppm)
+        d = rtdump.load(full)
+        s = d["sums"]
+        rows = np.arange(0, H, H // 8).astype(np.int32)
+        body = open(ppm, "rb").read()
+        header = b"P6\n%d %d\n255\n" % (W, H)
+        assert body.startswith(header)
+        u8 = np.frombuffer(body[len(header):], np.uint8).reshape(H, W, 3)
+        rtdump.save(out, {"row_fnv1a": row_hash(s), "rows": rows, "row_sums": s[rows], "row_u8": u8[rows],
+                          "counters": d["counters"]})
+        meta["frames"][name] = {"scene": scene, "width": W, "height": H, "spp": S, "file": os.path.basename(out),
+                                "frame_u8_sha1": hashlib.sha1(body[len(header):]).hexdigest(),
+                                "ppm_sha1": hashlib.sha1(body).hexdigest(), "sums": info,
+                                "scene_sha256": scene_sha256(scene)}
+        print(name, meta["frames"][name], flush=True)
+        save(meta)
+    # C5: seeded pixels of every rank's shard of the 8-way split (rank 0 has its own 256-pixel file)
+    name, scene, W, H, S, world, _ = CONFIGS[3]
+    out = os.path.join(GOLD, f"{name}_{scene}_pixels_{W}x{H}x{S}_w{world}_ranks1to7.rtd")
+    if not (os.path.exists(out) and "c5_ranks" in meta.get("configs", {})):
+        path = scenes.ensure_scene(scene, SCENE_DIR)
+        idx = np.concatenate([shard_pixels(W, H, world, r, C5_RANKS_PIXELS, 2000 + r) for r in range(1, world)])
+        lst = f"/tmp/{name}_ranks_idx.i64"
+        idx.tofile(lst)
+        meta.setdefault("configs", {})["c5_ranks"] = {
+            "scene": scene, "width": W, "height": H, "spp": S, "world": world, "ranks": list(range(1, world)),
+            "pixels_per_rank": C5_RANKS_PIXELS, "file": os.path.basename(out),
+            "pixels": harness("pixels", path, W, H, S, lst, out, threads)}
+        print("c5_ranks", meta["configs"]["c5_ranks"], flush=True)
+
+
 SHIPPED = [("cornell", 128, 128, 256), ("sponza_mini", 128, 72, 256)]
 
 
@@ -174,6 +220,15 @@ def main():
         shipped_goldens(meta)
         with open(path, "w") as f:
             json.dump(meta, f, indent=1, sort_keys=True)
+        return
+    if "--frames" in sys.argv:
+        path = os.path.join(GOLD, "golden_meta.json")
+        meta = json.load(open(path))
+        def save(m):
+            with open(path, "w") as f:
+                json.dump(m, f, indent=1, sort_keys=True)
+        frame_goldens(meta, save)
+        save(meta)
         return
     if "--configs" in sys.argv:
         path = os.path.join(GOLD, "golden_meta.json")
