@@ -67,7 +67,13 @@ constexpr int kShadeMin = RT_SHADE_MIN;
 #ifndef RT_INNER_TRAV
 #define RT_INNER_TRAV 1
 #endif
-constexpr bool kInnerTrav = RT_INNER_TRAV != 0;   // a wave shades once this many lanes are READY (or none traverses)
+constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
+// ... whose leaf work is spread over the wave (rt_wavefront.h trav_step_coop).  0: per-lane
+// leaf steps of RT_LEAF_N triangles, for A/B builds.
+#ifndef RT_COOP_LEAF
+#define RT_COOP_LEAF 1
+#endif
+constexpr bool kCoopLeaf = RT_COOP_LEAF != 0;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -102,6 +108,8 @@ constexpr double kWfCompactBelow = 0.75;   // wavefront: dense queue until this 
 struct rt_device_blob {
     std::vector<uint8_t> bytes;
     size_t o_tri, o_attr, o_tan, o_node, o_light, o_lnode, o_mf, o_mt, o_nt, o_ti, o_tx, o_lut;
+    size_t o_node_soa = 0, o_tri_soa = 0;   // RT_SOA builds only
+    long long node_plane = 0, tri_plane = 0;
 };
 
 struct rt_device_scene {
@@ -342,7 +350,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             // change: the outer loop's work between two shading passes is only this.
             int kt = nt;
             do {
-                if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) L.state = rtd::M_READY;
+                if (kCoopLeaf) {
+                    if (rtd::trav_step_coop<COUNT>(sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV)) L.state = rtd::M_READY;
+                } else if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) {
+                    L.state = rtd::M_READY;
+                }
                 const unsigned long long rb = __ballot(L.state == rtd::M_READY), tb = __ballot(L.state == rtd::M_TRAV);
                 kt = __popcll(tb);
                 if (kt == 0 || __popcll(rb) >= (kSpec ? kSpecShadeMin : kShadeMin)) break;
@@ -671,6 +683,24 @@ int ensure_blob(rt_scene *s) {
     std::vector<float> lut(512);
     rtd::fill_decode_lut(lut.data());
     b->o_lut = append(blob, lut);
+#if RT_SOA
+    {   // SoA planes of the BFS nodes and of the triangles (the coop traversal step reads these)
+        const std::vector<float> bn = rtd::bfs_nodes(s->node);
+        const size_t nn = bn.size() / 8, nt = s->tri.size() / 12;
+        const long long np = (long long)((nn + 3) & ~size_t(1)), tp = (long long)nt;
+        std::vector<float> ns((size_t)np * 2 * 4, 0.f), ts((size_t)std::max<long long>(tp, 1) * 3 * 4, 0.f);
+        for (size_t k = 0; k < nn; ++k) {
+            std::memcpy(&ns[4 * (1 + k)], &bn[8 * k], 4 * sizeof(float));
+            std::memcpy(&ns[4 * ((size_t)np + 1 + k)], &bn[8 * k + 4], 4 * sizeof(float));
+        }
+        for (size_t k = 0; k < nt; ++k)
+            for (int pl = 0; pl < 3; ++pl) std::memcpy(&ts[4 * ((size_t)pl * tp + k)], &s->tri[12 * k + 4 * pl], 4 * sizeof(float));
+        b->o_node_soa = append(blob, ns);
+        b->o_tri_soa = append(blob, ts);
+        b->node_plane = np;
+        b->tri_plane = tp;
+    }
+#endif
     blob.resize(((blob.size() + 255) & ~size_t(255)) + 256);
     s->blob = b;
     return RT_OK;
@@ -726,6 +756,10 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.tex_info = (const uint4 *)(base + b.o_ti);
     ds.texels = (const uint32_t *)(base + b.o_tx);
     ds.lut = (const float *)(base + b.o_lut);
+    ds.node_soa = b.o_node_soa ? (const float4 *)(base + b.o_node_soa) : nullptr;
+    ds.tri_soa = b.o_tri_soa ? (const float4 *)(base + b.o_tri_soa) : nullptr;
+    ds.node_plane = b.node_plane;
+    ds.tri_plane = b.tri_plane;
     ds.n_lights = (int)(s->light.size() / 16);
     ds.n_tris = (int)(s->tri.size() / 12);
     ds.n_nodes = (int)(s->node.size() / 8);

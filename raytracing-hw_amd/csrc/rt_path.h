@@ -101,6 +101,12 @@ struct DevScene {
     const uint4 *tex_info;    // texel offset, width, height, channels
     const uint32_t *texels;   // RGBA8
     const float *lut;         // 512: [b] = sRGB decode powf(b / 255.f, 2.2f), [256 + b] = b / 255.f
+    // RT_SOA A/B builds only: the traversal's node and triangle records as
+    // planes of float4 (node: (min, max.x) | (max.yz, a, b) at index 1 + id; triangle:
+    // (v0, U.x) | (U.yz, V.xy) | (V.z, n_geo)), plane strides in float4; null otherwise
+    const float4 *node_soa;
+    const float4 *tri_soa;
+    long long node_plane, tri_plane;
     int n_lights;
     int n_tris, n_nodes, n_meshes;
     int ray_depth;

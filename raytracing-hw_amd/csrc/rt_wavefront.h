@@ -379,6 +379,41 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
     }
 }
 
+// The node part of a traversal step: the child pair q[0..3] (two 32-B node records) of the
+// internal node T is entering; pushes the far child when both are hit, enters the near one
+// (or the far one alone, or returns: T.phase = TP_POP).
+template <bool COUNT, class Stack>
+__device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravState &T, Stack &stk, Counters &cnt) {
+    NodeRec L, R;
+    L.mn[0] = q[0].x; L.mn[1] = q[0].y; L.mn[2] = q[0].z; L.mx[0] = q[0].w; L.mx[1] = q[1].x; L.mx[2] = q[1].y;
+    L.a = __float_as_uint(q[1].z); L.b = __float_as_uint(q[1].w);
+    R.mn[0] = q[2].x; R.mn[1] = q[2].y; R.mn[2] = q[2].z; R.mx[0] = q[2].w; R.mx[1] = q[3].x; R.mx[2] = q[3].y;
+    R.a = __float_as_uint(q[3].z); R.b = __float_as_uint(q[3].w);
+    if (COUNT) cnt.aabb += 2;
+    // dir[split axis] > 0: left child first (sign bits recomputed: cheaper than a register)
+    const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
+    const bool lf = (dpos >> T.b) & 1u;
+    // test both boxes as they are stored, then name them near / far
+    float cF[3];
+    bool hL, hR, inF;
+    box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
+    const float ef = box_dist(cF, inF, r);   // the far child's entry distance
+    const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
+    const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
+    if (hn && hf) {
+        RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
+        stk.put(T.sp++, make_uint2((fa << 10) | fb, __float_as_uint(ef)));
+#ifdef RT_STACK_PROBE
+        RT_STACK_PROBE(T.sp);
+#endif
+    }
+    // near child; or, the near box missed, the far child unless its entry distance
+    // exceeds the node's local best (still 1e9); or return
+    const bool far_only = !hn && hf && !(ef > 1e9f);
+    if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
+    else T.phase = TP_POP;
+}
+
 // One unit of traversal work: the child pair of one internal node, or RT_LEAF_N triangles
 // of a leaf, followed (when the subtree is finished) by the return up the frames until a
 // far child is to be visited.  Returns true once the stack is empty (T.best is final).  A
@@ -414,34 +449,7 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
 #endif
     }
     if (at_node) {
-        NodeRec L, R;
-        L.mn[0] = q[0].x; L.mn[1] = q[0].y; L.mn[2] = q[0].z; L.mx[0] = q[0].w; L.mx[1] = q[1].x; L.mx[2] = q[1].y;
-        L.a = __float_as_uint(q[1].z); L.b = __float_as_uint(q[1].w);
-        R.mn[0] = q[2].x; R.mn[1] = q[2].y; R.mn[2] = q[2].z; R.mx[0] = q[2].w; R.mx[1] = q[3].x; R.mx[2] = q[3].y;
-        R.a = __float_as_uint(q[3].z); R.b = __float_as_uint(q[3].w);
-        if (COUNT) cnt.aabb += 2;
-        // dir[split axis] > 0: left child first (sign bits recomputed: cheaper than a register)
-        const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
-        const bool lf = (dpos >> T.b) & 1u;
-        // test both boxes as they are stored, then name them near / far
-        float cF[3];
-        bool hL, hR, inF;
-        box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
-        const float ef = box_dist(cF, inF, r);   // the far child's entry distance
-        const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
-        const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
-        if (hn && hf) {
-            RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
-            stk.put(T.sp++, make_uint2((fa << 10) | fb, __float_as_uint(ef)));
-#ifdef RT_STACK_PROBE
-            RT_STACK_PROBE(T.sp);
-#endif
-        }
-        // near child; or, the near box missed, the far child unless its entry distance
-        // exceeds the node's local best (still 1e9); or return
-        const bool far_only = !hn && hf && !(ef > 1e9f);
-        if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
-        else T.phase = TP_POP;
+        node_step<COUNT>(q, r, T, stk, cnt);
     } else if (at_leaf) {
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -496,6 +504,132 @@ struct LdsStack {
         return v;
     }
 };
+
+// Cooperative traversal step (the lane-resident kernel's inner loop, GPU only).  A wave's
+// lanes are mostly at internal nodes, a few at leaves, and a per-lane step runs both code
+// paths for the whole wave: the leaf path (RT_LEAF_N triangles, ~200 instructions) for a
+// sixth of the work.  Here the leaf work is spread over the wave instead: each leaf lane
+// (the first kCoopLeaves of them, by lane order) publishes its ray and triangle range in LDS,
+// and lanes 4h .. 4h+3 of the wave, whatever their own state, test triangles k .. k+3 of the
+// h-th leaf lane, one each.  A quad reduction finds the first of the hits with the least t
+// (Primitive::intersect's strict <, bvh.cpp:226-232, in index order), which the leaf lane
+// takes; so a leaf of up to 4 triangles is one step, with the reference's winner and local
+// best.  Node lanes run node_step as in trav_step.  Every lane of the wave must call this
+// (active: the lane is traversing); returns true once the lane's stack is empty.
+#ifndef RT_SOA
+#define RT_SOA 0   // 1: SoA node / triangle planes for the coop step (A/B build)
+#endif
+#ifndef RT_COOP_LEAVES
+#define RT_COOP_LEAVES 16
+#endif
+constexpr int kCoopLeaves = RT_COOP_LEAVES;   // leaf lanes served per step (4 lanes of the wave each)
+static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
+__shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)
+
+// One step of the quad reduction: take the partner lane's (t, u, v, index) when its t is
+// less, or equal with a lower index.
+template <int CTL>
+__device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, int &cj) {
+    const float c2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(c), CTL, 0xF, 0xF, false));
+    const float u2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cu), CTL, 0xF, 0xF, false));
+    const float v2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cv), CTL, 0xF, 0xF, false));
+    const int j2 = __builtin_amdgcn_mov_dpp(cj, CTL, 0xF, 0xF, false);
+    const bool take = c2 < c || (c2 == c && j2 < cj);
+    c = take ? c2 : c;
+    cu = take ? u2 : cu;
+    cv = take ? v2 : cv;
+    cj = take ? j2 : cj;
+}
+
+template <bool COUNT, class Stack, class Nodes>
+__device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
+                                               const Nodes &nodes, Counters &cnt, bool active) {
+    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+    const bool at_node = active && T.phase == TP_NODE, at_leaf = active && T.phase == TP_LEAF;
+    RT_CHECK(!at_node || T.a + 1 < (uint32_t)sc.n_nodes, 10, T.a, T.a = 0);
+    RT_CHECK(!at_leaf || T.kend <= (uint32_t)sc.n_tris, 12, T.kend, T.k = T.kend = 1);
+    // node lanes: the child pair (issued first; consumed after the leaf exchange)
+    float4 q[4];
+#if RT_SOA
+    {   // (A/B layout: two planes, the pair's halves 32 B apart in each)
+        const float4 *p0 = sc.node_soa + 1 + (size_t)(at_node ? T.a : 0u), *p1 = p0 + sc.node_plane;
+        q[0] = p0[0];
+        q[2] = p0[1];
+        q[1] = p1[0];
+        q[3] = p1[1];
+    }
+#else
+    {
+        const float4 *p0 = nodes.pair(at_node ? T.a : 0u);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = p0[i];
+    }
+#endif
+    // leaf lanes publish (rank = position among the wave's leaf lanes)
+    const unsigned long long lm = __ballot(at_leaf);
+    if (lm) {   // (wave-uniform)
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+        const bool served = at_leaf && rank < kCoopLeaves;
+        if (served) {
+            wf_coop_rec[wave][rank][0] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float(T.k));
+            wf_coop_rec[wave][rank][1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(T.kend));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int n_served = __popcll(lm) < kCoopLeaves ? __popcll(lm) : kCoopLeaves;
+        // helper lanes: one triangle each
+        const int h = lane >> 2, j = lane & 3;
+        float c = __builtin_inff(), cu = 0.f, cv = 0.f;
+        if (h < n_served) {
+            const float4 a = wf_coop_rec[wave][h][0], b = wf_coop_rec[wave][h][1];
+            const uint32_t k = __float_as_uint(a.w) + (uint32_t)j;
+            if (k < __float_as_uint(b.w)) {
+#if RT_SOA
+                const float4 *t = sc.tri_soa + (size_t)k;
+                const float4 t0 = t[0], t1 = t[sc.tri_plane], t2 = t[2 * sc.tri_plane];
+#else
+                const float4 *t = sc.tri + 3 * (size_t)k;
+                const float4 t0 = t[0], t1 = t[1], t2 = t[2];
+#endif
+                Ray hr;
+                hr.o = V3{a.x, a.y, a.z};
+                hr.d = V3{b.x, b.y, b.z};
+                TriHit th;
+                // (a NaN t never wins a strict < : it becomes "no hit" here)
+                if (tri_hit_bl(V3{t0.x, t0.y, t0.z}, V3{t0.w, t1.x, t1.y}, V3{t1.z, t1.w, t2.x}, hr, th) &&
+                    th.t == th.t) {
+                    c = th.t;
+                    cu = th.u;
+                    cv = th.v;
+                }
+            }
+        }
+        // quad reduction: least t, first triangle of equal t; every lane of the quad ends
+        // with it (DPP quad permutes: lane ^ 1, then lane ^ 2)
+        int cj = j;
+        quad_min_step<0xB1>(c, cu, cv, cj);   // quad_perm [1,0,3,2]: lane ^ 1
+        quad_min_step<0x4E>(c, cu, cv, cj);   // quad_perm [2,3,0,1]: lane ^ 2
+        const int src = 4 * (rank < kCoopLeaves ? rank : 0);
+        const float wc = __shfl(c, src, 64), wu = __shfl(cu, src, 64), wv = __shfl(cv, src, 64);
+        const int wj = __shfl(cj, src, 64);
+        if (served) {
+            if (COUNT) cnt.tri += (T.kend - T.k < 4u ? T.kend - T.k : 4u);
+            if (wc < T.acc) T.acc = wc;
+            if (wc < T.best.t) {
+                T.best.t = wc;
+                T.best.u = wu;
+                T.best.v = wv;
+                T.best.prim = (int)(T.k + (uint32_t)wj);
+            }
+            T.k += 4u;
+            if (T.k >= T.kend) T.phase = TP_POP;
+        }
+    }
+    // node lanes: the pair test
+    if (at_node) node_step<COUNT>(q, r, T, stk, cnt);
+    if (active && T.phase == TP_POP) return trav_pop(T, stk);
+    return false;
+}
 
 #endif
 

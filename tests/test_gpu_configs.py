@@ -134,7 +134,7 @@ def test_c5_ranks_1_to_7_match_reference(gpu):
     assert checked == len(g["index"]) == 64 * len(c["ranks"])
 
 
-@pytest.mark.parametrize("config", ["c3", "headline"])
+@pytest.mark.parametrize("config", sorted(FRAMES))
 def test_whole_frame_matches_reference(gpu, config):
     """The whole BASELINE frame against the reference's own render of it (scene.cpp:31-64):
     every row's FNV-1a hash of the float sums, 8 full rows bit for bit, and the sha1 of the
