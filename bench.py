@@ -401,8 +401,16 @@ def main():
         traffic_frac = None if traffic is None else traffic / avg_s / 1e9 / HBM_PEAK_GBS
         # the label follows the counters: HBM-bound only when the measured HBM-side traffic is
         # at least half of what the algorithmic model asks for
-        bound = ("hbm (algorithmic model only: no PMC pass)" if traffic_frac is None
-                 else "hbm" if traffic_frac >= 0.5 * frac else "latency/issue")
+        # the label follows the counters: HBM-bound only when the measured
+        # HBM-side traffic is at least half of what the algorithmic model asks for and the
+        # memory side is busier than the issue side (VALU issue rate / the SIMD-32 ceiling)
+        issue_share = None if issue is None else issue["issue_frac_of_simd32_peak"]
+        if traffic_frac is None:
+            bound = "hbm (algorithmic model only: no PMC pass)"
+        elif traffic_frac < 0.5 * frac or (issue_share is not None and issue_share > traffic_frac):
+            bound = "latency/issue"
+        else:
+            bound = "hbm"
         ref_sha = reference_frame_sha1(args.scene, W, H, S)
         line = {
             "metric": "Mrays/sec + frame time, Sponza 1920x1080x256spp at 1/2/4/8 MI355X",

@@ -73,7 +73,16 @@ constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #ifndef RT_COOP_LEAF
 #define RT_COOP_LEAF 1
 #endif
-constexpr bool kCoopLeaf = RT_COOP_LEAF != 0;   // a wave shades once this many lanes are READY (or none traverses)
+constexpr bool kCoopLeaf = RT_COOP_LEAF != 0;
+// Leaf lanes a coop step serves (32 B of LDS per wave each).  The plain kernel's block is at
+// 30 KB and must stay within 32 KB minus what the runtime keeps, for 5 blocks per CU: 16
+// records (32 KB) measured 1426 ms against 1272 at 8 (4 blocks per CU).  The runahead kernel
+// runs 4 blocks per CU anyway (128 VGPRs): 16 there (8-way slowest shard 245 vs 249 ms).
+#ifndef RT_COOP_LEAVES
+#define RT_COOP_LEAVES 8
+#endif
+constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
+constexpr int kCoopLeavesSpec = 16;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -351,7 +360,9 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             int kt = nt;
             do {
                 if (kCoopLeaf) {
-                    if (rtd::trav_step_coop<COUNT>(sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV)) L.state = rtd::M_READY;
+                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain>(
+                            sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV))
+                        L.state = rtd::M_READY;
                 } else if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) {
                     L.state = rtd::M_READY;
                 }

@@ -519,12 +519,6 @@ struct LdsStack {
 #ifndef RT_SOA
 #define RT_SOA 0   // 1: SoA node / triangle planes for the coop step (A/B build)
 #endif
-#ifndef RT_COOP_LEAVES
-#define RT_COOP_LEAVES 16
-#endif
-constexpr int kCoopLeaves = RT_COOP_LEAVES;   // leaf lanes served per step (4 lanes of the wave each)
-static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
-__shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)
 
 // One step of the quad reduction: take the partner lane's (t, u, v, index) when its t is
 // less, or equal with a lower index.
@@ -541,9 +535,13 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
     cj = take ? j2 : cj;
 }
 
-template <bool COUNT, class Stack, class Nodes>
+// kCoopLeaves: leaf lanes served per step (4 lanes of the wave each); their records take
+// 32 B each per wave in LDS (the caller's kernel budget decides: DESIGN.md §6).
+template <bool COUNT, int kCoopLeaves, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active) {
+    static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
+    __shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)
     const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
     const bool at_node = active && T.phase == TP_NODE, at_leaf = active && T.phase == TP_LEAF;
     RT_CHECK(!at_node || T.a + 1 < (uint32_t)sc.n_nodes, 10, T.a, T.a = 0);
