@@ -27,10 +27,18 @@ roofline = rank 0's render kernel.  Default (kernel 0, lane-resident rt_mega_ker
            the guide's gfx950 correction), `traffic_undoubled` without the doubling and
            `traffic_frac` = traffic / launch time / peak.
 cpu_baseline: the reference itself (oracle/_ref/ref_render, built from /root/reference's
-           sources) timing its Scene::render loop on every host core (nproc threads) over a
-           bounded sample of the same frame (every 8th row, 16 spp); a counting build of the
-           same sources counts its rays.  Falls back to the build's CPU restatement (oracle/)
-           when _ref is absent.
+           sources) timing its Scene::render loop on the host cores this process may use
+           (min(nproc, cgroup CPU quota) threads; `cores` says how many) over a bounded sample
+           of the same frame (every 8th row, 16 spp); a counting build of the same sources
+           counts its rays.  Falls back to the build's CPU restatement (oracle/) when _ref is
+           absent.
+roofline.bound follows the committed counters: "latency/issue" when the HBM-side traffic
+           is under half the algorithmic model's or below the VALU issue utilisation
+           (roofline.issue: VALU instructions per SIMD-cycle from the SQ passes, lane
+           utilisation, SALU share, wait share), else "hbm".
+frame_matches_reference: the 8-bit frame's sha1 against the reference's own finished frame of
+           the same workload (tests/golden/golden_meta.json "frames"), computed after the timed
+           region.
 """
 import argparse
 import hashlib
@@ -205,7 +213,7 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=135, help="rows of the frame in the CPU baseline sample")
     ap.add_argument("--cpu-stride", type=int, default=8, help="CPU baseline sample: every n-th row")
     ap.add_argument("--cpu-spp", type=int, default=16)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = nproc)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(nproc, cgroup quota))")
     ap.add_argument("--natural-steps", type=int, default=1,
                     help="timed frames in row-major pixel order (no pre-pass), reported beside the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -72,7 +72,13 @@ constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;
 #ifndef RT_SPEC_ISOLATED
 #define RT_SPEC_ISOLATED 0
 #endif
-constexpr long long kSpecIsolated = RT_SPEC_ISOLATED;   // the runahead kernel's batch threshold
+constexpr long long kSpecIsolated = RT_SPEC_ISOLATED;
+// Runahead kernel: a tail wave also shades as soon as the frontier job of its heaviest pixel
+// (the record at lane 0) is ready, so that chain never waits for a batch (A/B builds).
+#ifndef RT_SPEC_CRIT
+#define RT_SPEC_CRIT 0
+#endif
+constexpr bool kSpecCrit = RT_SPEC_CRIT != 0;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;
 // Traversal iterations between two shading passes run as an inner loop of their own (no pixel
 // claim, runahead pass or schedule decision per iteration).  0: one iteration per pass of the
@@ -297,6 +303,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     bool exhausted = false;
     bool tail = false, wave_room = false;
     int rank_q = -1;   // runahead kernel: quartile of the wave's heaviest pixel among the shard's (0 = heaviest)
+    int crit = -1;     // runahead kernel (RT_SPEC_CRIT): lane running the frontier of the wave's heaviest pixel
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -339,6 +346,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 rtd::spec_convert(L, rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, lane);
                 tail = true;
                 wave_room = false;
+                if (kSpecCrit) crit = __shfl(L.pix, 0, 64) >= 0 ? 0 : -1;   // lane 0: the wave's heaviest pixel
 #ifdef RT_MEGA_PROF
                 if (lane == 0) RT_SPEC_STAT(7, 1);
 #endif
@@ -352,6 +360,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                     wave_room = rtd::spec_manage(rtd::SpecLanes{L}, sc, g,
                                                  rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, spp,
                                                  out, root);
+                    if (kSpecCrit) {   // the lane now running record 0's frontier job (table slot 0)
+                        const rtd::SpecView V{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane};
+                        const uint4 a0 = *V.w(0, 0), b0 = *V.w(1, 0), c0 = *V.w(2, 0);
+                        crit = (b0.w & rtd::kRecActive) && a0.z > a0.y ? (int)(c0.w & 63u) : -1;
+                    }
 #ifdef RT_MEGA_PROF
                     if (lane == 0) {
                         RT_SPEC_STAT(0, 1);
@@ -366,9 +379,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         } else if (!__any(L.pix >= 0)) {
             break;
         }
-        const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
+        const unsigned long long rmask = __ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY));
+        const int nr = __popcll(rmask);
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
-        const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0);
+        const bool crit_ready = kSpecCrit && crit >= 0 && ((rmask >> crit) & 1ull);
+        const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0 || crit_ready);
         // Runahead kernel (the 8-way shards): a traversal iteration issues at priority 1, a
         // shading pass at 0, so waves in their long shading code give issue slots to waves
         // stepping the frame's sample chains: slowest 8-way shard 295 -> 280 ms.  The plain
@@ -421,6 +436,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 const unsigned long long rb = __ballot(L.state == rtd::M_READY), tb = __ballot(L.state == rtd::M_TRAV);
                 kt = __popcll(tb);
                 if (kt == 0 || __popcll(rb) >= (kSpec ? kSpecShadeMin : kShadeMin)) break;
+                if (kSpecCrit && crit >= 0 && ((rb >> crit) & 1ull)) break;   // the wave's critical chain is ready
 #ifdef RT_MEGA_PROF
                 pf[4] += 1;
                 pf[6] += (unsigned long long)kt;

@@ -91,7 +91,8 @@ __device__ __forceinline__ void counters_flush(const Counters &c, unsigned long 
 //     has to wait for the near subtree;
 //   * frames are 8 bytes and carry the far child itself (its a/b fields and entry distance),
 //     so resuming a node never re-reads it:
-//       far frame  (a << 10 | b, entry distance)  pushed when both children are hit;
+//       far frame  (a << 10 | b, entry distance squared: box_dist2)  pushed when both
+//                                                  children are hit;
 //       best frame (kFrameAcc,  node's near best)  pushed when the far child is entered
 //                                                  after a near subtree.
 //     No frame is needed when a node has only one child to visit: its local best starts at
@@ -150,6 +151,29 @@ __device__ __forceinline__ float box_dist(const float coord[3], bool inside, con
     const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
     return inside ? 0.f : l;
 }
+// The same distance before its square root: length()'s sum of squares (vector.h:146-152),
+// 0 from inside.  sqrtf is correctly rounded and monotonic, so box_dist = sqrtf(box_dist2)
+// bit for bit; traversal frames carry the sum and take the root only when a comparison is
+// too close to call without it (sqrt_gt).
+__device__ __forceinline__ float box_dist2(const float coord[3], bool inside, const Ray &r) {
+    const V3 v = rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o);
+    float m = 0.f;
+    m += v.x * v.x;
+    m += v.y * v.y;
+    m += v.z * v.z;
+    return inside ? 0.f : m;
+}
+// sqrtf(s) > a, exactly, for a finite a >= 0 (a traversal bound) and any s (a sum from
+// box_dist2: >= 0 or NaN).  fl(a*a) scaled by 1 -+ 2^-14 brackets a^2 far beyond the rounding
+// of a*a, of the scaling and of sqrtf, so outside the bracket the answer is that of s against
+// a^2; inside it (or for a below 2^-40, where a*a loses precision) the root decides.
+__device__ __forceinline__ bool sqrt_gt(float s, float a) {
+    const float a2 = a * a;
+    const bool big = a >= 0x1p-40f;
+    if (big && s < a2 * 0x1.fffcp-1f) return false;
+    if (big && s > a2 * 0x1.0002p+0f) return true;
+    return sqrtf(s) > a;
+}
 template <bool DIST>
 __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], const Ray &r, float &dist) {
     float coord[3];
@@ -168,41 +192,45 @@ __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], co
 //     the only one whose distance traversal needs.
 __device__ __forceinline__ void box_pair_hit(const NodeRec &L, const NodeRec &R, const Ray &r, bool lf, bool &hL, bool &hR,
                                              float coordF[3], bool &insideF) {
+    // (the conditions are kept in positive form -- "outside the slab", "off the winning
+    // plane" -- so that few of them need a negation: each negation of a wave mask is a
+    // scalar instruction)
     const float o[3] = {r.o.x, r.o.y, r.o.z};
     const float d[3] = {r.d.x, r.d.y, r.d.z};
     const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
-    bool inL = true, inR = true;
+    bool anyL = false, anyR = false;   // some axis has the origin outside the slab (not inside)
     float candL[3], candR[3], mtL[3], mtR[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const bool loL = o[i] < L.mn[i], loR = o[i] < R.mn[i];
-        const bool midL = !loL & !(o[i] > L.mx[i]), midR = !loR & !(o[i] > R.mx[i]);
-        inL = inL & midL;
-        inR = inR & midR;
+        const bool outL = loL | (o[i] > L.mx[i]), outR = loR | (o[i] > R.mx[i]);   // quadrant != Mid
+        anyL = anyL | outL;
+        anyR = anyR | outR;
         candL[i] = loL ? L.mn[i] : L.mx[i];
         candR[i] = loR ? R.mn[i] : R.mx[i];
         const bool dnz = d[i] != 0.f;
         const float tL = (candL[i] - o[i]) * inv[i], tR = (candR[i] - o[i]) * inv[i];
-        mtL[i] = (!midL & dnz) ? tL : -1.f;
-        mtR[i] = (!midR & dnz) ? tR : -1.f;
+        mtL[i] = (outL & dnz) ? tL : -1.f;
+        mtR[i] = (outR & dnz) ? tR : -1.f;
     }
     const bool w1L = mtL[0] < mtL[1], w1R = mtR[0] < mtR[1];
     const float t01L = w1L ? mtL[1] : mtL[0], t01R = w1R ? mtR[1] : mtR[0];
     const bool w2L = t01L < mtL[2], w2R = t01R < mtR[2];
     const float twL = w2L ? mtL[2] : t01L, twR = w2R ? mtR[2] : t01R;
-    const bool onL[3] = {(bool)(!w1L & !w2L), (bool)(w1L & !w2L), w2L};
-    const bool onR[3] = {(bool)(!w1R & !w2R), (bool)(w1R & !w2R), w2R};
-    bool outL = twL < 0.f, outR = twR < 0.f;
+    // off the winning plane (whichPlane != i): axis 0 loses to 1 or 2, axis 1 loses to 0 or 2
+    const bool offL[3] = {(bool)(w1L | w2L), (bool)(!w1L | w2L), (bool)!w2L};
+    const bool offR[3] = {(bool)(w1R | w2R), (bool)(!w1R | w2R), (bool)!w2R};
+    bool missL = twL < 0.f, missR = twR < 0.f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float cL = o[i] + twL * d[i], cR = o[i] + twR * d[i];
-        outL = outL | (!onL[i] & ((cL < L.mn[i]) | (cL > L.mx[i])));
-        outR = outR | (!onR[i] & ((cR < R.mn[i]) | (cR > R.mx[i])));
-        coordF[i] = lf ? (onR[i] ? candR[i] : cR) : (onL[i] ? candL[i] : cL);
+        missL = missL | (offL[i] & ((cL < L.mn[i]) | (cL > L.mx[i])));
+        missR = missR | (offR[i] & ((cR < R.mn[i]) | (cR > R.mx[i])));
+        coordF[i] = lf ? (offR[i] ? cR : candR[i]) : (offL[i] ? cL : candL[i]);
     }
-    hL = inL || !outL;
-    hR = inR || !outR;
-    insideF = lf ? inR : inL;
+    hL = !(anyL & missL);   // inside, or the entry point lies on the box
+    hR = !(anyR & missR);
+    insideF = lf ? !anyR : !anyL;
 }
 
 // 1.f / x, correctly rounded, in three instructions where that is exact: the hardware
@@ -366,7 +394,7 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
             acc = acc < p ? acc : p;
             continue;
         }
-        if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
+        if (!sqrt_gt(__uint_as_float(f.y), acc)) {   // far child survives the near subtree's best
             stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
 #ifdef RT_STACK_PROBE
             RT_STACK_PROBE(sp);
@@ -397,7 +425,7 @@ __device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravS
     float cF[3];
     bool hL, hR, inF;
     box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
-    const float ef = box_dist(cF, inF, r);   // the far child's entry distance
+    const float ef = box_dist2(cF, inF, r);   // the far child's entry distance, squared (sqrt_gt)
     const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
     const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
     if (hn && hf) {
@@ -409,7 +437,7 @@ __device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravS
     }
     // near child; or, the near box missed, the far child unless its entry distance
     // exceeds the node's local best (still 1e9); or return
-    const bool far_only = !hn && hf && !(ef > 1e9f);
+    const bool far_only = !hn && hf && !sqrt_gt(ef, 1e9f);
     if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
     else T.phase = TP_POP;
 }
@@ -598,7 +626,7 @@ __device__ __forceinline__ void node_step2_coop(const DevScene &sc, const float4
             float cF[3];
             bool hL, hR, inF;
             box_pair_hit(Lr, Rr, hrr, lf, hL, hR, cF, inF);
-            ef = box_dist(cF, inF, hrr);
+            ef = box_dist2(cF, inF, hrr);
             flags = (int)(lf ? hL : hR) | (int)(lf ? hR : hL) << 1;   // near hit, far hit
         }
     }
@@ -618,7 +646,7 @@ __device__ __forceinline__ void node_step2_coop(const DevScene &sc, const float4
             RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
             stk.put(T.sp++, make_uint2((fa << 10) | fb, __float_as_uint(e0)));
         }
-        const bool far_only = !hn && hf && !(e0 > 1e9f);
+        const bool far_only = !hn && hf && !sqrt_gt(e0, 1e9f);
         if (hn || far_only) {
             const bool into_left = hn ? lf : !lf;
             trav_enter(T, hn ? na : fa, hn ? nb : fb);
@@ -637,7 +665,7 @@ __device__ __forceinline__ void node_step2_coop(const DevScene &sc, const float4
                     RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
                     stk.put(T.sp++, make_uint2((fa2 << 10) | fb2, __float_as_uint(el)));
                 }
-                const bool far_only2 = !hn2 && hf2 && !(el > 1e9f);
+                const bool far_only2 = !hn2 && hf2 && !sqrt_gt(el, 1e9f);
                 if (hn2 || far_only2) trav_enter(T, hn2 ? na2 : fa2, hn2 ? nb2 : fb2);
                 else T.phase = TP_POP;
             }
