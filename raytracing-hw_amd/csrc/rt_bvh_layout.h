@@ -49,20 +49,4 @@ inline std::vector<float> bfs_nodes(const std::vector<float> &node) {
     return out;
 }
 
-// The grandchildren of every sibling pair of a BFS node array (bfs_nodes): entry p (left
-// child 2p + 1, right child 2p + 2) is 16 floats of the left child's child pair, then 16 of
-// the right child's (zeros where the child is a leaf).  Node records are copied unchanged.
-inline std::vector<float> grand_pairs(const std::vector<float> &bfs) {
-    const size_t n = bfs.size() / 8, pairs = n > 1 ? (n - 1) / 2 : 0;
-    std::vector<float> g(pairs * 32 + 32, 0.f);
-    for (size_t p = 0; p < pairs; ++p)
-        for (int side = 0; side < 2; ++side) {
-            const size_t c = 2 * p + 1 + side;
-            if (node_word(bfs, c, 7) >= 3u) continue;   // leaf
-            const uint32_t a = node_word(bfs, c, 6);
-            std::memcpy(&g[32 * p + 16 * side], &bfs[8 * (size_t)a], 16 * sizeof(float));
-        }
-    return g;
-}
-
 }  // namespace rtd

@@ -52,11 +52,6 @@ constexpr int kMegaWpe = RT_MEGA_WPE;   // waves per SIMD the register allocatio
 #define RT_SPEC_WPE 4
 #endif
 constexpr int kMegaWpeSpec = RT_SPEC_WPE;
-// Runahead kernel wave priority: 0 by phase (traversal 1, shading 0); 1 by the cost rank of
-// the wave's heaviest pixel; 2 both (A/B builds).
-#ifndef RT_SPEC_PRIO
-#define RT_SPEC_PRIO 0
-#endif
 #ifndef RT_SHADE_MIN
 #define RT_SHADE_MIN 48
 #endif
@@ -67,18 +62,7 @@ constexpr int kMegaWpeSpec = RT_SPEC_WPE;
 #ifndef RT_SPEC_SHADE_MIN
 #define RT_SPEC_SHADE_MIN 32
 #endif
-constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;
-// Runahead kernel: waves that hold one heavy pixel each (rt_order_spread_kernel), 0 = none.
-#ifndef RT_SPEC_ISOLATED
-#define RT_SPEC_ISOLATED 0
-#endif
-constexpr long long kSpecIsolated = RT_SPEC_ISOLATED;
-// Runahead kernel: a tail wave also shades as soon as the frontier job of its heaviest pixel
-// (the record at lane 0) is ready, so that chain never waits for a batch (A/B builds).
-#ifndef RT_SPEC_CRIT
-#define RT_SPEC_CRIT 0
-#endif
-constexpr bool kSpecCrit = RT_SPEC_CRIT != 0;   // the runahead kernel's batch threshold
+constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;
 // Traversal iterations between two shading passes run as an inner loop of their own (no pixel
 // claim, runahead pass or schedule decision per iteration).  0: one iteration per pass of the
@@ -104,13 +88,7 @@ constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
 #ifndef RT_SPEC_COOP_LEAVES
 #define RT_SPEC_COOP_LEAVES 16
 #endif
-constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;
-// The runahead kernel takes two node levels per step while at most 16 of a wave's lanes are
-// at internal nodes (rt_wavefront.h node_step2_coop).  0: one level, for A/B builds.
-#ifndef RT_TWO_LEVEL
-#define RT_TWO_LEVEL 0
-#endif
-constexpr bool kTwoLevel = RT_TWO_LEVEL != 0;   // a wave shades once this many lanes are READY (or none traverses)
+constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -145,7 +123,6 @@ constexpr double kWfCompactBelow = 0.75;   // wavefront: dense queue until this 
 struct rt_device_blob {
     std::vector<uint8_t> bytes;
     size_t o_tri, o_attr, o_tan, o_node, o_light, o_lnode, o_mf, o_mt, o_nt, o_ti, o_tx, o_lut;
-    size_t o_grand = 0;                     // rt_bvh_layout.h grand_pairs
     size_t o_node_soa = 0, o_tri_soa = 0;   // RT_SOA builds only
     long long node_plane = 0, tri_plane = 0;
 };
@@ -280,11 +257,9 @@ __device__ unsigned int g_wave_n;
 template <bool COUNT, bool FAST = false, bool LSPLIT = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPEC ? kMegaWpeSpec : kMegaWpe, 8)))
 rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
-               unsigned long long *queue, const int *order, unsigned *cost, int cs, long long iso) {
+               unsigned long long *queue, const int *order, unsigned *cost, int cs) {
     constexpr bool kSpec = SPEC && !COUNT && !FAST && !LSPLIT;
-    // iso (runahead kernel with an order): items [0, 64 iso) are iso waves' claims of one pixel
-    // and 63 empty items (order < 0) each; a wave that claims one starts its tail at once
-    const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels + iso * 63;
+    const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels;
     const int lane = threadIdx.x & 63;
     // texel-decode LUT in LDS: the shading's lane-dependent lookups become ds_reads
     __shared__ float lut[512];
@@ -302,8 +277,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     L.state = rtd::M_IDLE;
     bool exhausted = false;
     bool tail = false, wave_room = false;
-    int rank_q = -1;   // runahead kernel: quartile of the wave's heaviest pixel among the shard's (0 = heaviest)
-    int crit = -1;     // runahead kernel (RT_SPEC_CRIT): lane running the frontier of the wave's heaviest pixel
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -321,23 +294,14 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 unsigned long long base = 0;
                 if (lane == leader) base = atomicAdd(queue, (unsigned long long)cm);
                 base = __shfl(base, leader, 64);
-                if (kSpec && rank_q < 0) {
-                    // the wave's first claim: with the heaviest-first spread order its lane 0
-                    // holds the pixel of cost rank base / 64, the wave's heaviest (launch_order)
-                    const long long nw = (long long)gridDim.x * 4;
-                    rank_q = (int)std::min<long long>(3, ((long long)base / 64) * 4 / (nw > 0 ? nw : 1));
-                }
                 if (need) {
                     const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
                     if (p < n_items) {
                         if (FAST) rtd::mega_assign_fast<COUNT>(L, sc, g, p, cs, spp, root, cnt);
-                        else {
-                            const int px = order ? order[p] : (int)p;
-                            if (px >= 0) rtd::mega_assign<COUNT>(L, sc, g, px, root, cnt);
-                        }
+                        else rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
                     }
                 }
-                if ((long long)base + cm >= n_items || (long long)base < iso * 64) exhausted = true;
+                if ((long long)base + cm >= n_items) exhausted = true;
             }
         }
         if constexpr (kSpec) {
@@ -346,7 +310,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 rtd::spec_convert(L, rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, lane);
                 tail = true;
                 wave_room = false;
-                if (kSpecCrit) crit = __shfl(L.pix, 0, 64) >= 0 ? 0 : -1;   // lane 0: the wave's heaviest pixel
 #ifdef RT_MEGA_PROF
                 if (lane == 0) RT_SPEC_STAT(7, 1);
 #endif
@@ -360,11 +323,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                     wave_room = rtd::spec_manage(rtd::SpecLanes{L}, sc, g,
                                                  rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, spp,
                                                  out, root);
-                    if (kSpecCrit) {   // the lane now running record 0's frontier job (table slot 0)
-                        const rtd::SpecView V{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane};
-                        const uint4 a0 = *V.w(0, 0), b0 = *V.w(1, 0), c0 = *V.w(2, 0);
-                        crit = (b0.w & rtd::kRecActive) && a0.z > a0.y ? (int)(c0.w & 63u) : -1;
-                    }
 #ifdef RT_MEGA_PROF
                     if (lane == 0) {
                         RT_SPEC_STAT(0, 1);
@@ -379,36 +337,17 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         } else if (!__any(L.pix >= 0)) {
             break;
         }
-        const unsigned long long rmask = __ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY));
-        const int nr = __popcll(rmask);
+        const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
-        const bool crit_ready = kSpecCrit && crit >= 0 && ((rmask >> crit) & 1ull);
-        const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0 || crit_ready);
+        const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0);
         // Runahead kernel (the 8-way shards): a traversal iteration issues at priority 1, a
         // shading pass at 0, so waves in their long shading code give issue slots to waves
         // stepping the frame's sample chains: slowest 8-way shard 295 -> 280 ms.  The plain
         // kernel stays at 0 (1 GPU: 1360 -> 1395 ms with the same toggle; 4-way unchanged)
         // (profiles/r02_tail_ab.jsonl).
         if constexpr (kSpec) {
-#if RT_SPEC_PRIO == 1
-            // by the cost rank of the wave's heaviest pixel: the waves holding the longest
-            // sample chains issue first on their SIMD (rank quartile 0 -> priority 3)
-            const int pr = rank_q < 0 ? 0 : 3 - rank_q;
-            __builtin_amdgcn_s_setprio((short)0);
-            if (pr == 3) __builtin_amdgcn_s_setprio(3);
-            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-#elif RT_SPEC_PRIO == 2
-            // rank and phase: traversal 3 / 2 / 1 / 1 by rank quartile, shading 0
-            const int pr = shade_now ? 0 : (rank_q <= 0 ? 3 : rank_q == 1 ? 2 : 1);
-            __builtin_amdgcn_s_setprio((short)0);
-            if (pr == 3) __builtin_amdgcn_s_setprio(3);
-            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-#else
             if (shade_now) __builtin_amdgcn_s_setprio(0);
             else __builtin_amdgcn_s_setprio(1);
-#endif
         }
 #ifdef RT_MEGA_PROF
         {
@@ -427,7 +366,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             int kt = nt;
             do {
                 if (kCoopLeaf) {
-                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain, kSpec && kTwoLevel>(
+                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain>(
                             sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV))
                         L.state = rtd::M_READY;
                 } else if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) {
@@ -436,7 +375,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 const unsigned long long rb = __ballot(L.state == rtd::M_READY), tb = __ballot(L.state == rtd::M_TRAV);
                 kt = __popcll(tb);
                 if (kt == 0 || __popcll(rb) >= (kSpec ? kSpecShadeMin : kShadeMin)) break;
-                if (kSpecCrit && crit >= 0 && ((rb >> crit) & 1ull)) break;   // the wave's critical chain is ready
 #ifdef RT_MEGA_PROF
                 pf[4] += 1;
                 pf[6] += (unsigned long long)kt;
@@ -510,26 +448,17 @@ __global__ void __launch_bounds__(256) rt_order_box_kernel(const unsigned *in, u
 // r = j * a + min(j, b) + gi (m = a * per + b: the ranks in (lane j, wave gi) order of the
 // items that exist).  A heavy pixel's wave-mates are then light and finish early, and its
 // sequential sample chain runs in a sparse wave.  Later claims stay heaviest-first.
-// iso > 0 (runahead kernel): the first iso waves' claims hold one pixel each, the iso
-// heaviest, and per - 1 empty items (-1): such a wave runs its one long chain with the rest
-// of its lanes free for that chain's runahead, on its own bounce rhythm; the other pixels are
-// spread as above over the remaining groups - iso waves, from item iso * per on.
 __global__ void __launch_bounds__(256) rt_order_spread_kernel(const int *sorted, int *order, long long n,
-                                                              long long groups, long long per, long long iso) {
+                                                              long long groups, long long per) {
     const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n + iso * (per - 1)) return;
-    if (q < iso * per) {
-        order[q] = q % per == 0 ? sorted[q / per] : -1;
-        return;
-    }
-    const long long q2 = q - iso * per, n2 = n - iso, g2 = groups - iso;
-    const long long m = n2 < g2 * per ? n2 : g2 * per;
-    long long r = q2;
-    if (q2 < m) {
-        const long long gi = q2 / per, j = q2 % per, a = m / per, b = m % per;
+    if (q >= n) return;
+    const long long m = n < groups * per ? n : groups * per;
+    long long r = q;
+    if (q < m) {
+        const long long gi = q / per, j = q % per, a = m / per, b = m % per;
         r = j * a + (j < b ? j : b) + gi;
     }
-    order[q] = sorted[iso + r];
+    order[q] = sorted[r];
 }
 
 // ------------------------------------------------------------------------ wavefront (kernel 4)
@@ -756,11 +685,7 @@ int ensure_blob(rt_scene *s) {
     b->o_tri = append(blob, s->tri);
     b->o_attr = append(blob, s->tri_attr);
     b->o_tan = append(blob, s->tri_tan);
-    {
-        const std::vector<float> bfs = rtd::bfs_nodes(s->node);
-        b->o_node = append(blob, bfs, 32);
-        b->o_grand = append(blob, rtd::grand_pairs(bfs));
-    }
+    b->o_node = append(blob, rtd::bfs_nodes(s->node), 32);
     b->o_light = append(blob, s->light);
     b->o_lnode = append(blob, s->light_node);
     b->o_mf = append(blob, s->mesh_f);
@@ -848,7 +773,6 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.tex_info = (const uint4 *)(base + b.o_ti);
     ds.texels = (const uint32_t *)(base + b.o_tx);
     ds.lut = (const float *)(base + b.o_lut);
-    ds.grand = (const float4 *)(base + b.o_grand);
     ds.node_soa = b.o_node_soa ? (const float4 *)(base + b.o_node_soa) : nullptr;
     ds.tri_soa = b.o_tri_soa ? (const float4 *)(base + b.o_tri_soa) : nullptr;
     ds.node_plane = b.node_plane;
@@ -1007,19 +931,18 @@ int launch_wavefront(rt_device_scene *d, const ShardGeom &g, int spp, int depth,
 // `groups` waves.  Results never depend on the order; it only shortens the
 // frame's tail.  Returns the order in d_order.
 int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, long long groups, long long per,
-                 long long iso, int **d_order) {
+                 int **d_order) {
     const long long n = g.n_pixels;
     // order buffer: cost, cost sorted, ids, ids sorted, order (n each), then the sort's scratch
     size_t tmp_bytes = 0;
     HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp_bytes, (unsigned *)nullptr, (unsigned *)nullptr,
                                                          (int *)nullptr, (int *)nullptr, (int)n, 0, 32, stream));
     const size_t arr = (((size_t)n * 4 + 255) / 256) * 256;
-    const size_t arr_order = ((((size_t)n + (size_t)iso * (size_t)(per - 1)) * 4 + 255) / 256) * 256;
-    HIP_TRY(grow(&d->order_buf, &d->order_bytes, 4 * arr + arr_order + tmp_bytes));
+    HIP_TRY(grow(&d->order_buf, &d->order_bytes, 5 * arr + tmp_bytes));
     uint8_t *b = (uint8_t *)d->order_buf;
     unsigned *cost = (unsigned *)b, *cost_sorted = (unsigned *)(b + arr);
     int *ids = (int *)(b + 2 * arr), *sorted = (int *)(b + 3 * arr), *order = (int *)(b + 4 * arr);
-    void *tmp = b + 4 * arr + arr_order;
+    void *tmp = b + 5 * arr;
     HIP_TRY(grow((void **)&d->fast_part, &d->fast_part_bytes, (size_t)n * 3 * sizeof(float)));
     HIP_TRY(hipMemsetAsync(d->queue + 1, 0, sizeof(unsigned long long), stream));
     auto pre = rt_mega_kernel<true, true>;
@@ -1028,7 +951,7 @@ int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, lon
     w.n = n;
     w.lanes = (long long)blocks * 256;
     hipLaunchKernelGGL(pre, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, kOrderSpp, d->fast_part,
-                       d->counters + 8, d->queue + 1, (const int *)nullptr, cost, kOrderSpp, 0LL);
+                       d->counters + 8, d->queue + 1, (const int *)nullptr, cost, kOrderSpp);
     HIP_TRY(hipGetLastError());
     const unsigned nb = (unsigned)((n + 255) / 256);
     if (kOrderRadius > 0) {   // box-filtered costs: the pixel's neighbourhood estimates its expected work
@@ -1042,9 +965,8 @@ int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, lon
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, cost, cost_sorted, ids, sorted, (int)n, 0, 32,
                                                          stream));
-    const long long n_items = n + iso * (per - 1);
-    hipLaunchKernelGGL(rt_order_spread_kernel, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream,
-                       (const int *)sorted, order, n, groups, per, iso);
+    hipLaunchKernelGGL(rt_order_spread_kernel, dim3(nb), dim3(256), 0, stream, (const int *)sorted, order, n, groups,
+                       per);
     HIP_TRY(hipGetLastError());
     *d_order = order;
     return RT_OK;
@@ -1120,10 +1042,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             w.n = g.n_pixels;
             w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity)
             int *order = nullptr;
-            long long iso = 0;   // runahead kernel: waves holding one heavy pixel each (launch_order)
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
-                iso = spec ? std::min<long long>(kSpecIsolated, std::min<long long>(g.n_pixels, 4LL * blocks / 2)) : 0;
-                rc = launch_order(d, g, stream, 4LL * blocks, 64, iso, &order);
+                rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
                 if (rc) return rc;
                 ordered = true;
             }
@@ -1143,7 +1063,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
-                               (const int *)order, (unsigned *)nullptr, cs, iso);
+                               (const int *)order, (unsigned *)nullptr, cs);
             HIP_TRY(hipGetLastError());
             if (fast) {
                 const long long n3 = g.n_pixels * 3;

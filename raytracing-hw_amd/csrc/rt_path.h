@@ -104,10 +104,6 @@ struct DevScene {
     // RT_SOA A/B builds only: the traversal's node and triangle records as
     // planes of float4 (node: (min, max.x) | (max.yz, a, b) at index 1 + id; triangle:
     // (v0, U.x) | (U.yz, V.xy) | (V.z, n_geo)), plane strides in float4; null otherwise
-    // grandchildren of each sibling pair (left child 2p + 1, right 2p + 2): 8 x float4 at
-    // [8 p]: the child pair of the left child, then that of the right (zero where a child is a
-    // leaf); the runahead kernel's two-level node steps read them (rt_wavefront.h)
-    const float4 *grand;
     const float4 *node_soa;
     const float4 *tri_soa;
     long long node_plane, tri_plane;

@@ -91,8 +91,7 @@ __device__ __forceinline__ void counters_flush(const Counters &c, unsigned long 
 //     has to wait for the near subtree;
 //   * frames are 8 bytes and carry the far child itself (its a/b fields and entry distance),
 //     so resuming a node never re-reads it:
-//       far frame  (a << 10 | b, entry distance squared: box_dist2)  pushed when both
-//                                                  children are hit;
+//       far frame  (a << 10 | b, entry distance)  pushed when both children are hit;
 //       best frame (kFrameAcc,  node's near best)  pushed when the far child is entered
 //                                                  after a near subtree.
 //     No frame is needed when a node has only one child to visit: its local best starts at
@@ -150,29 +149,6 @@ __device__ __forceinline__ bool box_hit_pt(const float mn[3], const float mx[3],
 __device__ __forceinline__ float box_dist(const float coord[3], bool inside, const Ray &r) {
     const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
     return inside ? 0.f : l;
-}
-// The same distance before its square root: length()'s sum of squares (vector.h:146-152),
-// 0 from inside.  sqrtf is correctly rounded and monotonic, so box_dist = sqrtf(box_dist2)
-// bit for bit; traversal frames carry the sum and take the root only when a comparison is
-// too close to call without it (sqrt_gt).
-__device__ __forceinline__ float box_dist2(const float coord[3], bool inside, const Ray &r) {
-    const V3 v = rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o);
-    float m = 0.f;
-    m += v.x * v.x;
-    m += v.y * v.y;
-    m += v.z * v.z;
-    return inside ? 0.f : m;
-}
-// sqrtf(s) > a, exactly, for a finite a >= 0 (a traversal bound) and any s (a sum from
-// box_dist2: >= 0 or NaN).  fl(a*a) scaled by 1 -+ 2^-14 brackets a^2 far beyond the rounding
-// of a*a, of the scaling and of sqrtf, so outside the bracket the answer is that of s against
-// a^2; inside it (or for a below 2^-40, where a*a loses precision) the root decides.
-__device__ __forceinline__ bool sqrt_gt(float s, float a) {
-    const float a2 = a * a;
-    const bool big = a >= 0x1p-40f;
-    if (big && s < a2 * 0x1.fffcp-1f) return false;
-    if (big && s > a2 * 0x1.0002p+0f) return true;
-    return sqrtf(s) > a;
 }
 template <bool DIST>
 __device__ __forceinline__ bool box_hit(const float mn[3], const float mx[3], const Ray &r, float &dist) {
@@ -394,7 +370,7 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
             acc = acc < p ? acc : p;
             continue;
         }
-        if (!sqrt_gt(__uint_as_float(f.y), acc)) {   // far child survives the near subtree's best
+        if (!(__uint_as_float(f.y) > acc)) {   // far child survives the near subtree's best
             stk.put(sp++, make_uint2(kFrameAcc, __float_as_uint(acc)));
 #ifdef RT_STACK_PROBE
             RT_STACK_PROBE(sp);
@@ -425,7 +401,7 @@ __device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravS
     float cF[3];
     bool hL, hR, inF;
     box_pair_hit(L, R, r, lf, hL, hR, cF, inF);
-    const float ef = box_dist2(cF, inF, r);   // the far child's entry distance, squared (sqrt_gt)
+    const float ef = box_dist(cF, inF, r);   // the far child's entry distance
     const bool hn = lf ? hL : hR, hf = lf ? hR : hL;
     const uint32_t na = lf ? L.a : R.a, nb = lf ? L.b : R.b, fa = lf ? R.a : L.a, fb = lf ? R.b : L.b;
     if (hn && hf) {
@@ -437,7 +413,7 @@ __device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravS
     }
     // near child; or, the near box missed, the far child unless its entry distance
     // exceeds the node's local best (still 1e9); or return
-    const bool far_only = !hn && hf && !sqrt_gt(ef, 1e9f);
+    const bool far_only = !hn && hf && !(ef > 1e9f);
     if (hn || far_only) trav_enter(T, hn ? na : fa, hn ? nb : fb);
     else T.phase = TP_POP;
 }
@@ -563,122 +539,9 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
     cj = take ? j2 : cj;
 }
 
-// Two node levels per step for a sparse wave (at most kTwoLevelLanes lanes at internal nodes;
-// the runahead kernel's tails, where a few long sample chains set the frame time).  Each
-// node lane gets three helper lanes of its wave: one tests the lane's child pair (L, R) as
-// node_step would, the other two test the child pairs of L and of R, read from the
-// grandchild array (DevScene::grand) at addresses that need no record of L or R, so all
-// three loads issue at once.  The node lane then takes node_step's decisions for its node
-// and, if it entered an internal child, for that child too, with the tests already done: the
-// same visits, pushes, frames and counters as two node_steps, one memory round trip instead
-// of two.  Every lane of the wave must call this (the shuffles); q: the lane's child pair.
-#ifndef RT_TWO_LEVEL_LANES
-#define RT_TWO_LEVEL_LANES 16
-#endif
-constexpr int kTwoLevelLanes = RT_TWO_LEVEL_LANES;
-static_assert(kTwoLevelLanes >= 1 && kTwoLevelLanes <= 16, "four helper lanes per node lane");
-
-template <bool COUNT, class Stack>
-__device__ __forceinline__ void node_step2_coop(const DevScene &sc, const float4 q[4], const Ray &r, TravState &T,
-                                                Stack &stk, Counters &cnt, bool at_node, unsigned long long nm) {
-    __shared__ uint8_t wf_two_owner[4][kTwoLevelLanes];
-    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
-    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
-    if (at_node) wf_two_owner[wave][rank] = (uint8_t)lane;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int n = __popcll(nm), hr = lane >> 2, part = lane & 3;
-    const bool hact = hr < n && part < 3;
-    const int src = hact ? (int)wf_two_owner[wave][hr] : lane;
-    // the owner's ray and node (every lane takes part in the shuffles)
-    Ray hrr;
-    hrr.o = V3{__shfl(r.o.x, src, 64), __shfl(r.o.y, src, 64), __shfl(r.o.z, src, 64)};
-    hrr.d = V3{__shfl(r.d.x, src, 64), __shfl(r.d.y, src, 64), __shfl(r.d.z, src, 64)};
-    hrr.inv = V3{__shfl(r.inv.x, src, 64), __shfl(r.inv.y, src, 64), __shfl(r.inv.z, src, 64)};
-    const uint32_t ta = (uint32_t)__shfl((int)T.a, src, 64), tb = (uint32_t)__shfl((int)T.b, src, 64);
-    // the owner's grandchild (a, b) fields: the second float4 of each of the four records
-    const float4 *gown = sc.grand + 8 * (size_t)(at_node ? (T.a - 1u) >> 1 : 0u);
-    const float4 g1 = gown[1], g3 = gown[3], g5 = gown[5], g7 = gown[7];
-    int flags = 0;
-    float ef = 0.f;
-    if (hact) {
-        float4 h[4];
-        uint32_t split = tb;
-        bool valid = true;
-        if (part == 0) {
-            const float4 *pp = sc.node + 2 * (size_t)ta;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) h[i] = pp[i];
-        } else {
-            const float4 pc = sc.node[2 * (size_t)ta + (part == 1 ? 1 : 3)];   // the child's (max.yz, a, b)
-            const float4 *g = sc.grand + 8 * (size_t)((ta - 1u) >> 1) + 4 * (part - 1);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) h[i] = g[i];
-            split = __float_as_uint(pc.w);
-            valid = split < 3u;   // an internal child: its pair is in the grandchild entry
-        }
-        if (valid) {
-            NodeRec Lr, Rr;
-            Lr.mn[0] = h[0].x; Lr.mn[1] = h[0].y; Lr.mn[2] = h[0].z; Lr.mx[0] = h[0].w; Lr.mx[1] = h[1].x; Lr.mx[2] = h[1].y;
-            Rr.mn[0] = h[2].x; Rr.mn[1] = h[2].y; Rr.mn[2] = h[2].z; Rr.mx[0] = h[2].w; Rr.mx[1] = h[3].x; Rr.mx[2] = h[3].y;
-            const uint32_t dpos = (hrr.d.x > 0.f ? 1u : 0u) | (hrr.d.y > 0.f ? 2u : 0u) | (hrr.d.z > 0.f ? 4u : 0u);
-            const bool lf = (dpos >> split) & 1u;
-            float cF[3];
-            bool hL, hR, inF;
-            box_pair_hit(Lr, Rr, hrr, lf, hL, hR, cF, inF);
-            ef = box_dist2(cF, inF, hrr);
-            flags = (int)(lf ? hL : hR) | (int)(lf ? hR : hL) << 1;   // near hit, far hit
-        }
-    }
-    const int b0 = 4 * (at_node ? rank : 0);
-    const int f0 = __shfl(flags, b0, 64), f1 = __shfl(flags, b0 + 1, 64), f2 = __shfl(flags, b0 + 2, 64);
-    const float e0 = __shfl(ef, b0, 64), e1 = __shfl(ef, b0 + 1, 64), e2 = __shfl(ef, b0 + 2, 64);
-    if (at_node) {
-        const uint32_t dpos = (r.d.x > 0.f ? 1u : 0u) | (r.d.y > 0.f ? 2u : 0u) | (r.d.z > 0.f ? 4u : 0u);
-        // level 1: node_step's decisions for T's node with (L, R) tested by helper 0
-        const uint32_t la = __float_as_uint(q[1].z), lb = __float_as_uint(q[1].w);
-        const uint32_t ra = __float_as_uint(q[3].z), rb = __float_as_uint(q[3].w);
-        if (COUNT) cnt.aabb += 2;
-        const bool lf = (dpos >> T.b) & 1u;
-        const bool hn = f0 & 1, hf = (f0 >> 1) & 1;
-        const uint32_t na = lf ? la : ra, nb = lf ? lb : rb, fa = lf ? ra : la, fb = lf ? rb : lb;
-        if (hn && hf) {
-            RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
-            stk.put(T.sp++, make_uint2((fa << 10) | fb, __float_as_uint(e0)));
-        }
-        const bool far_only = !hn && hf && !sqrt_gt(e0, 1e9f);
-        if (hn || far_only) {
-            const bool into_left = hn ? lf : !lf;
-            trav_enter(T, hn ? na : fa, hn ? nb : fb);
-            if (T.phase == TP_NODE) {
-                // level 2: the entered child's pair, tested by helper 1 (left child) or 2 (right)
-                if (COUNT) cnt.aabb += 2;
-                const int fl = into_left ? f1 : f2;
-                const float el = into_left ? e1 : e2;
-                const float4 ga = into_left ? g1 : g5, gb = into_left ? g3 : g7;   // grandchildren (a, b)
-                const bool lf2 = (dpos >> T.b) & 1u;
-                const bool hn2 = fl & 1, hf2 = (fl >> 1) & 1;
-                const uint32_t a0 = __float_as_uint(ga.z), b0f = __float_as_uint(ga.w);
-                const uint32_t a1 = __float_as_uint(gb.z), b1f = __float_as_uint(gb.w);
-                const uint32_t na2 = lf2 ? a0 : a1, nb2 = lf2 ? b0f : b1f, fa2 = lf2 ? a1 : a0, fb2 = lf2 ? b1f : b0f;
-                if (hn2 && hf2) {
-                    RT_CHECK(T.sp < kStack, 11, T.sp, T.sp = 0);
-                    stk.put(T.sp++, make_uint2((fa2 << 10) | fb2, __float_as_uint(el)));
-                }
-                const bool far_only2 = !hn2 && hf2 && !sqrt_gt(el, 1e9f);
-                if (hn2 || far_only2) trav_enter(T, hn2 ? na2 : fa2, hn2 ? nb2 : fb2);
-                else T.phase = TP_POP;
-            }
-        } else {
-            T.phase = TP_POP;
-        }
-    }
-}
-
 // kCoopLeaves: leaf lanes served per step (4 lanes of the wave each); their records take
-// 32 B each per wave in LDS (the caller's kernel budget decides: DESIGN.md §6).  TWO_LEVEL:
-// node_step2_coop when the wave is sparse.
-template <bool COUNT, int kCoopLeaves, bool TWO_LEVEL, class Stack, class Nodes>
+// 32 B each per wave in LDS (the caller's kernel budget decides: DESIGN.md §6).
+template <bool COUNT, int kCoopLeaves, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active) {
     static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
@@ -764,14 +627,8 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
             if (T.k >= T.kend) T.phase = TP_POP;
         }
     }
-    // node lanes: the pair test (two levels in a sparse wave)
-    if (TWO_LEVEL) {
-        const unsigned long long nm = __ballot(at_node);
-        if (nm && __popcll(nm) <= kTwoLevelLanes) node_step2_coop<COUNT>(sc, q, r, T, stk, cnt, at_node, nm);
-        else if (at_node) node_step<COUNT>(q, r, T, stk, cnt);
-    } else if (at_node) {
-        node_step<COUNT>(q, r, T, stk, cnt);
-    }
+    // node lanes: the pair test
+    if (at_node) node_step<COUNT>(q, r, T, stk, cnt);
     if (active && T.phase == TP_POP) return trav_pop(T, stk);
     return false;
 }

@@ -402,39 +402,3 @@ extern "C" long long kh_box_pair_check(long long n, uint32_t seed) {
     }
     return bad;
 }
-
-// sqrt_gt (rt_wavefront.h: the traversal's culling test on the squared entry distance)
-// against sqrtf(s) > a on n cases: a from hit distances across the float range (zero, tiny,
-// ordinary, 1e9), s at and around a * a (every float within 64 ulp of it), and random s.
-// Returns the number of disagreements.
-extern "C" long long kh_sqrt_gt_check(long long n, uint32_t seed) {
-    uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
-    auto next = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
-    auto bitsf = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
-    auto fbits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
-    long long bad = 0;
-    for (long long k = 0; k < n; ++k) {
-        const uint64_t r = next();
-        float a;
-        switch (r & 7) {
-            case 0: a = 0.f; break;
-            case 1: a = 1e9f; break;
-            case 2: a = bitsf((uint32_t)(next() % 0x7f800000u)); break;     // any finite non-negative float
-            case 3: a = bitsf((uint32_t)(next() % 0x2b800000u)); break;     // tiny (below 2^-40)
-            default: a = (float)((next() >> 40) & 0xffffff) * 0x1p-12f; break;   // 0 .. 4096
-        }
-        float s;
-        const float a2 = a * a;
-        switch ((r >> 3) & 3) {
-            case 0: s = bitsf(fbits(a2) + (uint32_t)(int32_t)((int)((next() & 127)) - 64)); break;
-            case 1: s = a2 * (1.f + (float)((int)(next() & 1023) - 512) * 0x1p-22f); break;   // within 2^-13 of a^2
-            case 2: s = bitsf((uint32_t)(next() % 0x7f800001u)); break;   // up to +inf
-            default: s = (next() & 15) == 0 ? __builtin_nanf("") : (float)((next() >> 40) & 0xffffff) * 0x1p-4f; break;
-        }
-        if (s != s || s >= 0.f) {
-            const bool want = std::sqrt(s) > a, got = rtd::sqrt_gt(s, a);
-            bad += want != got;
-        }
-    }
-    return bad;
-}

@@ -39,8 +39,6 @@ def _build_kh(tmp_path_factory, *defines):
     lib.kh_render_mega_lsplit.restype = I
     lib.kh_box_pair_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
     lib.kh_box_pair_check.restype = ctypes.c_int64
-    lib.kh_sqrt_gt_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
-    lib.kh_sqrt_gt_check.restype = ctypes.c_int64
     return lib
 
 
@@ -245,14 +243,6 @@ def test_box_pair_matches_single_box_test(kh):
     primitive.cpp:146-208, restated op for op) on 4 M random cases rich in special values:
     signed zeros, infinities, NaN, flat and inverted boxes, planes through the origin."""
     assert kh.kh_box_pair_check(4_000_000, 7) == 0
-
-
-def test_sqrt_gt_matches_rooted_compare(kh):
-    """Traversal frames carry the far box's squared entry distance; sqrt_gt decides
-    sqrtf(s) > bound without the root except near the boundary.  It must equal the rooted
-    compare (bvh.cpp:190-197 `pre_inter.value() > intersection.distance`) on 4 M cases
-    packed around s = bound^2, tiny and huge bounds, zero, infinity and NaN."""
-    assert kh.kh_sqrt_gt_check(4_000_000, 11) == 0
 
 
 @pytest.mark.parametrize("name,w,h", [("cornell", 64, 64), ("cornell_blob", 48, 48), ("practice6_1", 64, 64),
