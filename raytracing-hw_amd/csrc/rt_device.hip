@@ -88,13 +88,7 @@ constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
 #ifndef RT_SPEC_COOP_LEAVES
 #define RT_SPEC_COOP_LEAVES 16
 #endif
-constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;
-// The runahead kernel prefetches both children's pairs of every node step into LDS
-// (rt_wavefront.h trav_step_coop PREFETCH).  A/B switch.
-#ifndef RT_SPEC_PREFETCH
-#define RT_SPEC_PREFETCH 0
-#endif
-constexpr bool kSpecPrefetch = RT_SPEC_PREFETCH != 0;   // a wave shades once this many lanes are READY (or none traverses)
+constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // a wave shades once this many lanes are READY (or none traverses)
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -372,7 +366,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             int kt = nt;
             do {
                 if (kCoopLeaf) {
-                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain, kSpec && kSpecPrefetch>(
+                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain>(
                             sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV))
                         L.state = rtd::M_READY;
                 } else if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) {

@@ -457,6 +457,10 @@ inline unsigned long long g_spec_prof[8];   // host test harness
 constexpr uint32_t kRecActive = 1u;
 constexpr uint32_t kRecXf = 2u;
 constexpr int kSpecWindow = RT_SPEC_WINDOW;   // jobs in flight per pixel at most, frontier included (<= 10)
+#ifndef RT_SPEC_LAZY
+#define RT_SPEC_LAZY 0
+#endif
+constexpr bool kSpecLazy = RT_SPEC_LAZY != 0;   // spec_job_end: only frontier ends trigger a pass
 constexpr int kSpecIssue = RT_SPEC_ISSUE;     // runahead jobs a pixel gets per management pass
 static_assert(kSpecWindow >= 1 && kSpecWindow <= 10, "lane table holds 10 slots");
 // The lanes running jobs f, f+1, ...: 6-bit slots of a 64-bit table (planes 2 and 3 .w).
@@ -620,7 +624,11 @@ __device__ __forceinline__ void spec_job_end(MegaLane &L, const DevScene &sc, co
     }
     lane_sum_set(L, color);
     lane_ctr_set(L, c);
-    L.state = M_DONE_NEW;
+    // A frontier job's end needs a pass (its sample is added there and the chain goes on); a
+    // runahead job's result can only be used once the frontier reaches it, so with
+    // RT_SPEC_LAZY it waits as M_DONE for the next pass instead of triggering one.
+    const bool frontier = (j.x >> 6) == a.w && t == a.y;
+    L.state = (!kSpecLazy || frontier) ? M_DONE_NEW : M_DONE;
 }
 
 // One management pass of a tail wave: add ended frontier jobs in order, free the lanes of

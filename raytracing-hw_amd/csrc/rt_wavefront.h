@@ -541,11 +541,7 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
 
 // kCoopLeaves: leaf lanes served per step (4 lanes of the wave each); their records take
 // 32 B each per wave in LDS (the caller's kernel budget decides: DESIGN.md §6).
-// PREFETCH: once a node lane's child pair has arrived, it starts the loads of both children's
-// own pairs into a per-wave LDS sink (global_load_lds: no register holds them), so the next
-// step's pair load, which is one of the two, finds its line in the CU's cache.  For the
-// runahead kernel, whose long chains take one dependent load per step.
-template <bool COUNT, int kCoopLeaves, bool PREFETCH = false, class Stack, class Nodes>
+template <bool COUNT, int kCoopLeaves, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active) {
     static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
@@ -632,20 +628,7 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
         }
     }
     // node lanes: the pair test
-    if (at_node) {
-        if (PREFETCH) {
-            __shared__ uint32_t wf_pf_sink[4][2][64];
-            const uint32_t la = __float_as_uint(q[1].z), lb = __float_as_uint(q[1].w);
-            const uint32_t ra = __float_as_uint(q[3].z), rb = __float_as_uint(q[3].w);
-            if (lb < 3u)
-                __builtin_amdgcn_global_load_lds((const void *)nodes.pair(la),
-                                                 (void __attribute__((address_space(3))) *)&wf_pf_sink[wave][0][0], 4, 0, 0);
-            if (rb < 3u)
-                __builtin_amdgcn_global_load_lds((const void *)nodes.pair(ra),
-                                                 (void __attribute__((address_space(3))) *)&wf_pf_sink[wave][1][0], 4, 0, 0);
-        }
-        node_step<COUNT>(q, r, T, stk, cnt);
-    }
+    if (at_node) node_step<COUNT>(q, r, T, stk, cnt);
     if (active && T.phase == TP_POP) return trav_pop(T, stk);
     return false;
 }
