@@ -89,6 +89,21 @@ constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
 #define RT_SPEC_COOP_LEAVES 16
 #endif
 constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // a wave shades once this many lanes are READY (or none traverses)
+// Leaf rounds per coop step (rt_wavefront.h trav_step_coop round_min): a further round
+// while at least this many leaf lanes are unserved.  Plain kernel: 8 (sponza 1080p 1292 ->
+// 1278 ms against one round per step).  Runahead kernel: 4 on scenes of fewer than
+// kCoopRoundNodes BVH nodes, where most traversal steps are leaf steps (cornell 512x512x64,
+// 36 triangles: 26.8 -> 16.7 ms), one round per step on larger ones (the 8-way sponza
+// shards: 1% slower with rounds) (profiles/r03_ab.jsonl r03q-s).
+#ifndef RT_COOP_ROUND_MIN
+#define RT_COOP_ROUND_MIN 8
+#endif
+#ifndef RT_SPEC_COOP_ROUND_MIN
+#define RT_SPEC_COOP_ROUND_MIN 4
+#endif
+constexpr int kCoopRoundMinPlain = RT_COOP_ROUND_MIN;
+constexpr int kCoopRoundMinSpec = RT_SPEC_COOP_ROUND_MIN;   // small scenes
+constexpr int kCoopRoundNodes = 4096;
 // Pixel order pre-pass (launch_order).  Compile-time only, for A/B builds (make variant).
 // Measured on sponza 1080p x256spp (tools/order_ab.py, profiles/r02_order_ab.jsonl): 1 spp and
 // a 9 x 9 box filter (1399 ms, pre-pass 6.8 ms) against row-major order (1436 ms), 2 spp
@@ -367,7 +382,8 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             do {
                 if (kCoopLeaf) {
                     if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain>(
-                            sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV))
+                            sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV,
+                            kSpec ? st.round_min : kCoopRoundMinPlain))
                         L.state = rtd::M_READY;
                 } else if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) {
                     L.state = rtd::M_READY;
@@ -1041,6 +1057,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             rtd::WfState w = d->wf;
             w.n = g.n_pixels;
             w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity)
+            w.round_min = d->ds.n_nodes < kCoopRoundNodes ? kCoopRoundMinSpec : 65;
             int *order = nullptr;
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
                 rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);

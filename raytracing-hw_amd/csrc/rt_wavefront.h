@@ -32,6 +32,7 @@ __device__ __forceinline__ int shard_row(const ShardGeom &g, int k) {
 struct WfState {
     long long n;      // path slots (= pixels of the shard)
     int D;            // vertex records per slot (= ray_depth)
+    int round_min;    // runahead kernel: trav_step_coop's round_min (host: scene size)
     float4 *st;       // 2 per slot: (rng state bits, normal cache, meta bits, 0), (pixel sum, 0)
     float4 *rec_ab;   // AosRec: 2 per slot and vertex; LaneRec: 2 per vertex and lane slot
     float *rec_c;     //         1 per slot and vertex; LaneRec: alpha per vertex and lane slot
@@ -539,11 +540,15 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
     cj = take ? j2 : cj;
 }
 
-// kCoopLeaves: leaf lanes served per step (4 lanes of the wave each); their records take
+// kCoopLeaves: leaf lanes served per round (4 lanes of the wave each); their records take
 // 32 B each per wave in LDS (the caller's kernel budget decides: DESIGN.md §6).
+// round_min: unserved leaf lanes that start another round of the same step (> 64: one
+// round per step).  A wave mostly at leaves (a scene of a few dozen triangles, whose tree
+// is a few levels deep) otherwise serves kCoopLeaves of its leaf lanes per step and idles
+// the rest (rt_device.hip kCoopRoundMin*).
 template <bool COUNT, int kCoopLeaves, class Stack, class Nodes>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
-                                               const Nodes &nodes, Counters &cnt, bool active) {
+                                               const Nodes &nodes, Counters &cnt, bool active, int round_min) {
     static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
     __shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)
     const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
@@ -567,18 +572,24 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
         for (int i = 0; i < 4; ++i) q[i] = p0[i];
     }
 #endif
-    // leaf lanes publish (rank = position among the wave's leaf lanes)
+    // leaf lanes publish (rank = position among the wave's leaf lanes); round b serves
+    // ranks b*kCoopLeaves .. (b+1)*kCoopLeaves-1, and a further round runs while at least
+    // round_min leaf lanes are left unserved (a wave mostly at leaves: small scenes)
     const unsigned long long lm = __ballot(at_leaf);
-    if (lm) {   // (wave-uniform)
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-        const bool served = at_leaf && rank < kCoopLeaves;
+    const int n_leaf = __popcll(lm);
+    const int lrank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+    for (int base = 0; base < n_leaf; base += kCoopLeaves) {   // (wave-uniform)
+        if (base > 0 && n_leaf - base < round_min) break;
+        const int rank = lrank - base;
+        const bool served = at_leaf && rank >= 0 && rank < kCoopLeaves;
+        if (base > 0) __builtin_amdgcn_wave_barrier();   // (the last round's records are read)
         if (served) {
             wf_coop_rec[wave][rank][0] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float(T.k));
             wf_coop_rec[wave][rank][1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(T.kend));
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const int n_served = __popcll(lm) < kCoopLeaves ? __popcll(lm) : kCoopLeaves;
+        const int n_served = n_leaf - base < kCoopLeaves ? n_leaf - base : kCoopLeaves;
         // helper lanes: one triangle each
         const int h = lane >> 2, j = lane & 3;
         float c = __builtin_inff(), cu = 0.f, cv = 0.f;
@@ -611,7 +622,7 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
         int cj = j;
         quad_min_step<0xB1>(c, cu, cv, cj);   // quad_perm [1,0,3,2]: lane ^ 1
         quad_min_step<0x4E>(c, cu, cv, cj);   // quad_perm [2,3,0,1]: lane ^ 2
-        const int src = 4 * (rank < kCoopLeaves ? rank : 0);
+        const int src = 4 * (served ? rank : 0);
         const float wc = __shfl(c, src, 64), wu = __shfl(cu, src, 64), wv = __shfl(cv, src, 64);
         const int wj = __shfl(cj, src, 64);
         if (served) {
