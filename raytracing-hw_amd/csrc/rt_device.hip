@@ -130,6 +130,12 @@ constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units 
 #define RT_SPEC_PIXELS_PER_LANE 1
 #endif
 constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
+// Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
+// holds at most 64 / k pixels and the grid grows k-fold (lockstep study).
+#ifndef RT_CLAIM_STRIDE
+#define RT_CLAIM_STRIDE 1
+#endif
+constexpr int kClaimStride = RT_CLAIM_STRIDE;
 constexpr int kWfRefill = 8;         // wavefront extend: idle lanes before a wave refills
 constexpr unsigned kWfChunk = 64;    // wavefront extend: queue entries claimed per atomic
 constexpr double kWfCompactBelow = 0.75;   // wavefront: dense queue until this active fraction
@@ -301,7 +307,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #endif
     for (;;) {
         if (!exhausted) {   // lanes without work take the next items (one atomic per wave)
-            const bool need = L.pix < 0;
+            const bool need = L.pix < 0 && (kClaimStride == 1 || lane % kClaimStride == 0);
             const unsigned long long m = __ballot(need);
             if (m) {
                 const int leader = __ffsll((unsigned long long)m) - 1;
@@ -1046,12 +1052,12 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             // headline: 342 -> 304 ms; at 4-way, 2 pixels per lane, it measured no gain).
             const long long full_blocks = resident_blocks(d, rt_mega_kernel<false, false, false, true>);
             const bool spec = !fast && !lsplit && !count && !(p->flags & RT_FLAG_NO_RUNAHEAD) &&
-                              g.n_pixels <= kSpecPixelsPerLane * full_blocks * 256;
+                              g.n_pixels * kClaimStride <= kSpecPixelsPerLane * full_blocks * 256;
             auto mk = fast ? (count ? rt_mega_kernel<true, true> : rt_mega_kernel<false, true>)
                            : lsplit ? (count ? rt_mega_kernel<true, false, true> : rt_mega_kernel<false, false, true>)
                                     : count ? rt_mega_kernel<true>
                                             : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
-            const unsigned blocks = persistent_blocks(d, mk, n_items);
+            const unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
             int rc = ensure_wf(d, std::max<long long>(g.n_pixels, (long long)blocks * 256), s->ray_depth);   // vertex records
             if (rc) return rc;
             rtd::WfState w = d->wf;

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--off", type=int, default=1, help="also time with the runahead off")
     ap.add_argument("--max-ranks", type=int, default=0, help="time only the first ranks of each split (0 = all)")
     ap.add_argument("--full", type=int, default=1, help="also time the whole frame on one GPU")
+    ap.add_argument("--row-block", type=int, default=8, help="rows per interleaved block of the split")
+    ap.add_argument("--rank-stride", type=int, default=1, help="time every k-th rank only")
     args = ap.parse_args()
     rt = bench.import_pkg()
     path = bench.load_scenes_module().ensure_scene(args.scene, os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes"))
@@ -38,9 +40,9 @@ def main():
     res = {"lib": os.environ.get("RT_LIB", "default"), "scene": args.scene, "frame": [W, H, S]}
 
     def t(world, rank, steps, on):
-        out = torch.zeros(rtdist.max_shard_rows(H, world) * W * 3, dtype=torch.float32, device="cuda")
-        ms = [scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, stats=True,
-                                  runahead=on)["render_ms"] for _ in range(steps)]
+        out = torch.zeros(rtdist.max_shard_rows(H, world, args.row_block) * W * 3, dtype=torch.float32, device="cuda")
+        ms = [scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=args.row_block,
+                                  stats=True, runahead=on)["render_ms"] for _ in range(steps)]
         return min(ms)
 
     worlds = [int(x) for x in args.worlds.split(",")]
@@ -53,7 +55,7 @@ def main():
         if args.full:
             res[f"full_ms_{tag}"] = round(t(1, 0, args.steps, on), 1)
         for world in worlds:
-            sh = [t(world, r, 1, on) for r in range(min(world, args.max_ranks or world))]
+            sh = [t(world, r, 1, on) for r in range(0, min(world, args.max_ranks or world), args.rank_stride)]
             res[f"shard{world}_ms_{tag}"] = [round(x, 1) for x in sh]
             res[f"shard{world}_max_ms_{tag}"] = round(max(sh), 1)
             if args.full:
