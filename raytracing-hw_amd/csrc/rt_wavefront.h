@@ -353,17 +353,31 @@ __device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint3
     return (bits & 8u) == 0;
 }
 
+// Frames one step pops at most; the rest wait for the lane's next step (T.phase stays
+// TP_POP), so a lane that unwinds many frames no longer holds its whole wave in the pop
+// loop: sponza 1080p 1280 -> 1148 ms, slowest 8-way shard 246 -> 217 ms, C5 at 16 spp
+// 348 -> 308 ms; 1 pop: 1150 / 219 ms, 3: 1164 / 221 (profiles/r03_ab.jsonl r03y).  0: no cap.
+#ifndef RT_MAX_POPS
+#define RT_MAX_POPS 2
+#endif
+constexpr int kMaxPops = RT_MAX_POPS;
 // The return of trav_step: merge subtree bests upwards until a far child is to be visited
-// (enter it: false) or the stack is empty (T.best is final: true).
+// (enter it: false), the stack is empty (T.best is final: true) or kMaxPops frames are
+// popped (false, still TP_POP).
 template <class Stack>
 __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
     float acc = T.acc;
     int sp = T.sp;
-    for (;;) {
+    for (int n = 0;; ++n) {
         if (sp == 0) {
             T.sp = 0;
             T.acc = acc;
             return true;
+        }
+        if (kMaxPops > 0 && n == kMaxPops) {   // the rest next step (T.phase stays TP_POP)
+            T.sp = sp;
+            T.acc = acc;
+            return false;
         }
         const uint2 f = stk.get(--sp);
         if (f.x == kFrameAcc) {
