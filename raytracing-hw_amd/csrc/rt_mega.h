@@ -444,15 +444,19 @@ inline unsigned long long g_spec_prof[8];   // host test harness
 #endif
 
 // Record meta (plane 1 .w): bit 0 active, bit 1 X_f known (false until the wave's first job of
-// the pixel ends).  Window and issue rate measured on the 4- and 8-way shards of the headline
-// frame (profiles/r02_runahead_ab.jsonl): window 3 307 ms, 4 306, 6 316 (8-way); one runahead
-// job per pixel per pass 304.  Windows that adapt to a pixel's prediction hit rate (grow on a
-// hit, halve on a miss) measured 384: the pixels with long chains lost their runahead too.
+// the pixel ends).  Window and issue rate, slowest 8-way shard of the headline frame: with
+// the round-3 traversal (inner loop, coop leaves, pop cap) window 3 with both runahead jobs
+// issued in one pass 208 ms; window 4 one job per pass 218, two 213, three 211; window 2
+// 212-215; window 6 228 (profiles/r03_ab.jsonl r03ad-af).  Fewer speculative jobs in flight
+// waste fewer lanes on mispredicted chains and add less divergence to the wave.  (Round 2:
+// window 3 307 ms, 4 306, 6 316.)  Windows that adapt to a pixel's prediction hit rate (grow
+// on a hit, halve on a miss) measured 384 (round 2): the pixels with long chains lost their
+// runahead too.
 #ifndef RT_SPEC_WINDOW
-#define RT_SPEC_WINDOW 4
+#define RT_SPEC_WINDOW 3
 #endif
 #ifndef RT_SPEC_ISSUE
-#define RT_SPEC_ISSUE 1
+#define RT_SPEC_ISSUE 2
 #endif
 constexpr uint32_t kRecActive = 1u;
 constexpr uint32_t kRecXf = 2u;
