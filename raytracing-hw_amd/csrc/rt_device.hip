@@ -126,8 +126,11 @@ constexpr int kOrderRadius = RT_ORDER_RADIUS;  // box filter of the pre-pass cos
 // 1357 vs 1393 ms).
 constexpr int kOrderMinSpp = 128;
 constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units per pixel
+// Round 3 (runahead window 3): up to 2 pixels per lane, so the 4-way shards of the headline
+// (2 per lane) use it too: slowest 4-way shard 347.5 vs 358.7 ms; at 4 per lane (2-way)
+// 636 vs 625 (profiles/r03_ab.jsonl r03ah24).
 #ifndef RT_SPEC_PIXELS_PER_LANE
-#define RT_SPEC_PIXELS_PER_LANE 1
+#define RT_SPEC_PIXELS_PER_LANE 2
 #endif
 constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
 // Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
@@ -1049,7 +1052,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const bool lsplit = !fast && (p->flags & RT_FLAG_LIGHT_SPLIT) != 0;
             // Speculative sample runahead (rt_mega.h) where the frame is mostly tail: a shard of
             // at most kSpecPixelsPerLane pixels per resident lane (the 8-way split of the
-            // headline: 342 -> 304 ms; at 4-way, 2 pixels per lane, it measured no gain).
+            // headline: 342 -> 304 ms in round 2; at 4-way, 2 pixels per lane, 359 -> 348 ms in round 3).
             const long long full_blocks = resident_blocks(d, rt_mega_kernel<false, false, false, true>);
             const bool spec = !fast && !lsplit && !count && !(p->flags & RT_FLAG_NO_RUNAHEAD) &&
                               g.n_pixels * kClaimStride <= kSpecPixelsPerLane * full_blocks * 256;
