@@ -55,12 +55,13 @@ constexpr int kMegaWpeSpec = RT_SPEC_WPE;
 #ifndef RT_SHADE_MIN
 #define RT_SHADE_MIN 48
 #endif
-// The runahead kernel (8-way shards, about one pixel per lane) shades at 32 READY lanes: its
-// waves thin out early, and a heavy chain's lane waits less for its batch.  8-way slowest
-// shard 294 ms at 32 (three runs 293.6-294.7) against 297-299 at 48; 28 293, 36 297, 24 298,
-// 56 307 (profiles/r02_tail_ab.jsonl).
+// The runahead kernel (4- and 8-way shards) shades at 40 READY lanes: its waves thin out
+// early, and a heavy chain's lane waits less for its batch than at the plain kernel's 48.
+// Round 3 (window 3): slowest 8-way shard 207.5-207.7 ms at 40 against 208.6-211.7 at 32 and
+// 214.8 at 24, 4-way 346-347 vs 352-354 (profiles/r03_ab.jsonl r03ah, r03ai).  Round 2: 294 ms
+// at 32 against 297-299 at 48 (profiles/r02_tail_ab.jsonl).
 #ifndef RT_SPEC_SHADE_MIN
-#define RT_SPEC_SHADE_MIN 32
+#define RT_SPEC_SHADE_MIN 40
 #endif
 constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;
