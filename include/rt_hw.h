@@ -215,7 +215,9 @@ int rt_device_synchronize(void);
 /* Device self-check of hardware-dependent arithmetic the kernels rely on for exactness
  * (no reference counterpart; test entry).  which 0: the traversal's fast reciprocal
  * (rt_wavefront.h rcp_ieee) against IEEE division over every float with a normal
- * reciprocal; *mismatches = floats that differ (0 = exact). */
+ * reciprocal; which 1: the computed linear texel decode (rt_path.h unorm8) against
+ * (float)b / 255.f for every byte, and the packed LDS RNG word round trip over every minstd
+ * state; *mismatches = values that differ (0 = exact). */
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches);
 
 #ifdef __cplusplus

@@ -356,7 +356,8 @@ def device_count():
 
 def device_selfcheck(which=0):
     """rt_device_selfcheck: mismatches of the kernels' hardware-dependent exact arithmetic
-    (0: the fast reciprocal over every float with a normal reciprocal)."""
+    (0: the fast reciprocal over every float with a normal reciprocal; 1: the computed linear
+    texel decode over every byte and the packed LDS RNG word over every minstd state)."""
     n = ctypes.c_uint64(0)
     _check(lib().rt_device_selfcheck(which, ctypes.byref(n)))
     return int(n.value)

@@ -289,15 +289,17 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     constexpr bool kSpec = SPEC && !COUNT && !FAST && !LSPLIT;
     const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels;
     const int lane = threadIdx.x & 63;
-    // texel-decode LUT in LDS: the shading's lane-dependent lookups become ds_reads
-    __shared__ float lut[512];
-    for (int k = threadIdx.x; k < 512; k += blockDim.x) lut[k] = sc_in.lut[k];
+    // sRGB texel-decode table in LDS: the shading's lane-dependent lookups become ds_reads (the
+    // linear decode is computed: rt_path.h texel_decode)
+    __shared__ float lut[256];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) lut[k] = sc_in.lut[k];
     __syncthreads();
     DevScene sc = sc_in;
     sc.lut = lut;
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    uint2 spill[rtd::kStack - rtd::kLdsStack];
-    rtd::LdsStack S{spill};
+    constexpr int kK = kSpec ? rtd::kLdsStackSpec : rtd::kLdsStack;   // LDS stack frames of this kernel
+    uint2 spill[rtd::kStack - kK];
+    rtd::LdsStackT<kK> S{spill};
     const rtd::GlobalNodes nodes{sc.node};
     const rtd::NodeRec root = rtd::load_node(sc.node, 0);
     rtd::MegaLane L;
@@ -532,8 +534,8 @@ __global__ void __launch_bounds__(256) wf_extend_kernel(DevScene sc, const float
         *next_count = 0;                                 // the shade kernel's output queue
     }
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    uint2 spill[rtd::kStack - rtd::kLdsStack];
-    rtd::LdsStack S{spill};
+    uint2 spill[rtd::kStack - rtd::kLdsStackWf];
+    rtd::LdsStackT<rtd::kLdsStackWf> S{spill};
     const int lane = threadIdx.x & 63;
     const rtd::GlobalNodes nodes{sc.node};
     const rtd::NodeRec root = rtd::load_node(sc.node, 0);
@@ -1534,14 +1536,35 @@ __global__ void __launch_bounds__(256) rcp_check_kernel(unsigned long long *bad)
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
 }
 
+// rt_device_selfcheck 1: the computed linear texel decode (rt_path.h unorm8) against the IEEE
+// division (float)b / 255.f for every byte b, and the packed LDS RNG word (rt_mega.h
+// rng_word_pack) round trip over the state range and both normal-cache flags.
+__global__ void __launch_bounds__(256) decode_check_kernel(unsigned long long *bad) {
+    unsigned long long local = 0;
+    if (blockIdx.x == 0) {
+        const uint32_t b = threadIdx.x;
+        local += __float_as_uint(rtd::unorm8(b)) != __float_as_uint((float)b / 255.f);
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2147483647ull;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t x = (uint32_t)i, f = (uint32_t)(i & 1u);
+        uint32_t ux, uf;
+        rtd::rng_word_unpack(rtd::rng_word_pack(x, f), ux, uf);
+        local += (ux != x) | (uf != f);
+    }
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
+}
+
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
     if (!mismatches) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: null output");
-    if (which != 0) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
+    if (which != 0 && which != 1) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
     unsigned long long *d = nullptr;
     HIP_TRY(hipMalloc((void **)&d, sizeof *d));
     hipError_t e = hipMemset(d, 0, sizeof *d);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
+        if (which == 0) hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
+        else hipLaunchKernelGGL(decode_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
         e = hipGetLastError();
     }
     unsigned long long h = 0;

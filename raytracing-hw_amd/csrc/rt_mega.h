@@ -74,18 +74,28 @@ __device__ __forceinline__ void lane_sum_set(MegaLane &L, V3 v) { L.sum = v; }
 #endif
 
 // The lane's RNG state (minstd word, normal cache) lives in LDS between its uses (sample
-// start, shading), 3 KB per block, instead of three VGPRs held through the traversal.
+// start, shading), 2 KB per block, instead of three VGPRs held through the traversal.  The
+// minstd word is below 2^31 (modulus 2^31 - 1), so the cache flag (0 or 1) rides in its top
+// bit (rt_device_selfcheck 1 checks the round trip): the kilobyte saved, with the computed
+// linear texel decode's, pays for a twelfth LDS stack frame.
+__device__ __forceinline__ uint32_t rng_word_pack(uint32_t x, uint32_t saved_avail) { return x | saved_avail << 31; }
+__device__ __forceinline__ void rng_word_unpack(uint32_t w, uint32_t &x, uint32_t &saved_avail) {
+    x = w & 0x7fffffffu;
+    saved_avail = w >> 31;
+}
 #if defined(__HIPCC__)
-__shared__ uint32_t mega_lds_rng[3 * 256];
+__shared__ uint32_t mega_lds_rng[2 * 256];
 __device__ __forceinline__ Rng lane_rng(const MegaLane &) {
     const int t = threadIdx.x;
-    return Rng{mega_lds_rng[t], mega_lds_rng[256 + t], __uint_as_float(mega_lds_rng[512 + t])};
+    Rng r;
+    rng_word_unpack(mega_lds_rng[t], r.x, r.saved_avail);
+    r.saved = __uint_as_float(mega_lds_rng[256 + t]);
+    return r;
 }
 __device__ __forceinline__ void lane_rng_set(MegaLane &, const Rng &r) {
     const int t = threadIdx.x;
-    mega_lds_rng[t] = r.x;
-    mega_lds_rng[256 + t] = r.saved_avail;
-    mega_lds_rng[512 + t] = __float_as_uint(r.saved);
+    mega_lds_rng[t] = rng_word_pack(r.x, r.saved_avail);
+    mega_lds_rng[256 + t] = __float_as_uint(r.saved);
 }
 #else
 __device__ __forceinline__ Rng lane_rng(const MegaLane &L) { return L.rng; }

@@ -88,6 +88,25 @@ inline void fill_decode_lut(float *lut) {
     }
 }
 
+// (float)b / 255.f for a byte b, correctly rounded, in three instructions: b times the float
+// nearest 1/255 and one fma Newton correction, which rounds correctly for all 256 bytes
+// (checked on the device by rt_device_selfcheck 1 and on the host by tests/test_libm.py).
+__device__ __forceinline__ float unorm8(uint32_t b) {
+    constexpr float r = 0x1.010102p-8f;   // (float)(1 / 255)
+    const float x = (float)b, q = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.f, x), r, q);
+}
+// A texel byte's decode.  Device: the sRGB half of the table (the lane-resident kernel stages
+// only those 256 entries in LDS) and the linear decode computed; host: the whole table.
+__device__ __forceinline__ float texel_decode(const float *lut, uint32_t byte, bool srgb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float s = lut[byte], l = unorm8(byte);
+    return srgb ? s : l;
+#else
+    return lut[(srgb ? 0u : 256u) + byte];
+#endif
+}
+
 struct DevScene {
     const float4 *tri;        // 3 x float4 / triangle: (v0, U.x) (U.yz, V.xy) (V.z, n_geo)
     const float4 *tri_attr;   // 4 x float4 / triangle: normals, texcoords, mesh id
@@ -465,7 +484,7 @@ __device__ __forceinline__ V4 tex_sample_ti(const DevScene &sc, const uint4 ti, 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t byte = (texel[k] >> (8 * c)) & 0xffu;
-            v[k] = sc.lut[(srgb ? 0u : 256u) + byte];   // kSrgbLut[byte] or (float)(int)byte / 255.f
+            v[k] = texel_decode(sc.lut, byte, srgb);   // kSrgbLut[byte] or (float)(int)byte / 255.f
         }
         res[c] = v[0] * (1 - dx) * (1 - dy) + v[1] * (1 - dx) * dy + v[2] * dx * (1 - dy) + v[3] * dx * dy;
     }

@@ -498,24 +498,39 @@ __device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, Trav
 // leave L2 before they are read back).  K = 11 fills the lane-resident kernel's block to
 // 30 KB of LDS (5 blocks per CU still fit): sponza 1080p x256spp 1401 -> 1364 ms, WRITE_SIZE
 // 124 -> 101 B per ray at K = 10; K = 12 (32 KB) drops a block per CU (1544 ms)
-// (profiles/r02_lds_stack_ab.jsonl).
+// (profiles/r02_lds_stack_ab.jsonl).  Round 3: K = 8 costs 4% (1195 vs 1143 ms, r03s2).  The
+// lane-resident kernel's K = 12 fits in the same 31 KB since its RNG words and texel table
+// shrank by 1 KB each (rt_mega.h lane_rng, rt_path.h texel_decode).  The runahead kernel runs
+// 4 blocks per CU (40 KB each), so it holds RT_SPEC_LDS_STACK frames.  Each kernel has its
+// own array (lds_stack_frames<K>).
 #ifndef RT_LDS_STACK
-#define RT_LDS_STACK 11
+#define RT_LDS_STACK 12
+#endif
+#ifndef RT_SPEC_LDS_STACK
+#define RT_SPEC_LDS_STACK 15
 #endif
 constexpr int kLdsStack = RT_LDS_STACK;   // stack frames per lane in LDS (deeper ones spill to scratch)
-__shared__ uint2 wf_lds_stack[kLdsStack * 256];   // blocks of 256 threads
-struct LdsStack {
-    uint2 *spill;   // this thread's private overflow array (scratch), kStack - kLdsStack entries
+constexpr int kLdsStackSpec = RT_SPEC_LDS_STACK;   // the runahead kernel's
+constexpr int kLdsStackWf = 11;                    // the wavefront extend kernel's
+template <int K>
+__device__ __forceinline__ uint2 *lds_stack_frames() {
+    __shared__ uint2 frames[K * 256];   // blocks of 256 threads
+    return frames;
+}
+template <int K>
+struct LdsStackT {
+    static_assert(K >= 1 && K < kStack, "LDS frames");
+    uint2 *spill;   // this thread's private overflow array (scratch), kStack - K entries
     __device__ __forceinline__ void put(int i, uint2 v) {
-        if (i < kLdsStack) wf_lds_stack[i * 256 + threadIdx.x] = v;
-        else spill[i - kLdsStack] = v;
+        if (i < K) lds_stack_frames<K>()[i * 256 + threadIdx.x] = v;
+        else spill[i - K] = v;
     }
     __device__ __forceinline__ uint2 get(int i) const {
         uint2 v;
-        if (i < kLdsStack) {
-            v = wf_lds_stack[i * 256 + threadIdx.x];
+        if (i < K) {
+            v = lds_stack_frames<K>()[i * 256 + threadIdx.x];
         } else {
-            v = spill[i - kLdsStack];
+            v = spill[i - K];
             // keeps the two loads apart: merged, they become one flat load through a
             // selected pointer instead of a ds_read
             asm volatile("" : "+v"(v.x), "+v"(v.y));

@@ -402,3 +402,22 @@ extern "C" long long kh_box_pair_check(long long n, uint32_t seed) {
     }
     return bad;
 }
+
+// rt_path.h unorm8 (the device's computed linear texel decode) against (float)b / 255.f for
+// every byte, and rt_mega.h's packed LDS RNG word round trip on the state's extremes; returns
+// the mismatches.
+extern "C" long long kh_decode_check() {
+    long long bad = 0;
+    for (uint32_t b = 0; b < 256; ++b) {
+        const float a = rtd::unorm8(b), want = (float)b / 255.f;
+        bad += std::memcmp(&a, &want, 4) != 0;
+    }
+    const uint32_t xs[] = {0u, 1u, 2u, 48271u, 0x3fffffffu, 0x7ffffffdu, 0x7ffffffeu};
+    for (uint32_t x : xs)
+        for (uint32_t f = 0; f < 2; ++f) {
+            uint32_t ux, uf;
+            rtd::rng_word_unpack(rtd::rng_word_pack(x, f), ux, uf);
+            bad += (ux != x) | (uf != f);
+        }
+    return bad;
+}

@@ -315,6 +315,13 @@ def test_fast_reciprocal_is_exact(gpu):
     assert gpu.device_selfcheck(0) == 0
 
 
+def test_texel_decode_and_rng_word_are_exact(gpu):
+    """The computed linear texel decode (rt_path.h unorm8) equals (float)b / 255.f for every
+    byte, and the packed LDS RNG word round-trips for every minstd state and both cache flags,
+    on the device (rt_device_selfcheck 1)."""
+    assert gpu.device_selfcheck(1) == 0
+
+
 @pytest.mark.parametrize("name,w,h,s", CASES)
 def test_light_split_kernel(gpu, name, w, h, s):
     """Light-split kernel (rt_mega.h light_step; RT_FLAG_LIGHT_SPLIT, off by

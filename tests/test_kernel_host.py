@@ -39,6 +39,8 @@ def _build_kh(tmp_path_factory, *defines):
     lib.kh_render_mega_lsplit.restype = I
     lib.kh_box_pair_check.argtypes = [ctypes.c_int64, ctypes.c_uint32]
     lib.kh_box_pair_check.restype = ctypes.c_int64
+    lib.kh_decode_check.argtypes = []
+    lib.kh_decode_check.restype = ctypes.c_int64
     return lib
 
 
@@ -338,3 +340,12 @@ def test_runahead_without_lights(rt, kh):
     assert kh.kh_render_mega_spec(ctypes.addressof(v), s, 0, 1, 8, 5, 48, None, out.ctypes.data,
                                   np.zeros(7, np.uint64).ctypes.data) == 0
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
+
+
+def test_linear_texel_decode_and_rng_word(kh):
+    """rt_path.h unorm8 (b times the float nearest 1/255, one fma correction) equals the
+    division (float)b / 255.f the reference's linear texel decode does (primitive.h:172-215)
+    for every byte; the lane-resident kernel's packed RNG word (minstd state and normal-cache
+    flag in one LDS word) round-trips.  The device runs the same checks
+    (rt_device_selfcheck 1, tests/test_gpu_parity.py)."""
+    assert kh.kh_decode_check() == 0
