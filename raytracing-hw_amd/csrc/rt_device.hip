@@ -30,6 +30,7 @@
 
 #include "rt_path.h"
 #include "rt_wavefront.h"
+#include <type_traits>
 #include "rt_mega.h"
 #include "rt_quant_lut.h"
 #include "rt_scene.h"
@@ -72,6 +73,12 @@ constexpr int kShadeMin = RT_SHADE_MIN;
 #define RT_INNER_TRAV 1
 #endif
 constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
+// The lane-resident kernel's traversal state shares the node and leaf fields (rt_wavefront.h
+// TravStateU; the runahead kernel keeps TravState).  0: TravState everywhere, for A/B builds.
+#ifndef RT_PLAIN_TRAV_SHARED
+#define RT_PLAIN_TRAV_SHARED 1
+#endif
+constexpr bool kPlainTravShared = RT_PLAIN_TRAV_SHARED != 0;
 // ... whose leaf work is spread over the wave (rt_wavefront.h trav_step_coop).  0: per-lane
 // leaf steps of RT_LEAF_N triangles, for A/B builds.
 #ifndef RT_COOP_LEAF
@@ -302,7 +309,9 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     rtd::LdsStackT<kK> S{spill};
     const rtd::GlobalNodes nodes{sc.node};
     const rtd::NodeRec root = rtd::load_node(sc.node, 0);
-    rtd::MegaLane L;
+    // lane state: the runahead kernel keeps TravState, the others share the node / leaf fields
+    // (rt_wavefront.h TravStateU)
+    std::conditional_t<kSpec || !kPlainTravShared, rtd::MegaLane, rtd::MegaLaneU> L;
     L.pix = -1;
     L.state = rtd::M_IDLE;
     bool exhausted = false;

@@ -28,7 +28,6 @@ inline thread_local long long g_mega_slot = 0;
 inline long long mega_slot() { return g_mega_slot; }
 #endif
 
-using MegaTrav = TravState;
 __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return sc.node; }
 
 // M_LTRAV / M_LREADY: light-pdf walk as its own traversal (light-split kernel, below).
@@ -36,7 +35,8 @@ __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return
 // state until its pixel's frontier reaches it (speculative runahead, below).
 enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4, M_DONE_NEW = 5, M_DONE = 6 };
 
-struct MegaLane {
+template <class TS>
+struct MegaLaneT {
     int pix;         // shard pixel (slot), -1 = none (the host keeps shards below 2^31 pixels)
     uint32_t ctr;    // LaneCtr packed: sample (bits 0-19), depth budget (20-23), vertices (24-28)
     int state;
@@ -50,27 +50,35 @@ struct MegaLane {
     Rng rng;
     V3 sum;
     Ray r;
-    MegaTrav T;
+    TS T;
 };
+// The runahead kernel's lanes (and the host harness's spec emulation) keep TravState; the
+// lane-resident kernel's TravStateU (rt_wavefront.h).
+using MegaLane = MegaLaneT<TravState>;
+using MegaLaneU = MegaLaneT<TravStateU>;
 
 // The lane's pixel sum lives in LDS (3 KB per block) instead of three VGPRs that stay live
 // through the shading code; with the RNG state below in LDS too: 30 -> 17 spilled VGPRs at
 // the 96-VGPR budget, 1478 -> 1517 Mrays/s at 1080p x256spp, 8-way shard 325 -> 318 ms.
 #if defined(__HIPCC__)
 __shared__ float mega_lds_sum[3 * 256];
-__device__ __forceinline__ V3 lane_sum(const MegaLane &) {
+template <class ML>
+__device__ __forceinline__ V3 lane_sum(const ML &) {
     const int t = threadIdx.x;
     return V3{mega_lds_sum[t], mega_lds_sum[256 + t], mega_lds_sum[512 + t]};
 }
-__device__ __forceinline__ void lane_sum_set(MegaLane &, V3 v) {
+template <class ML>
+__device__ __forceinline__ void lane_sum_set(ML &, V3 v) {
     const int t = threadIdx.x;
     mega_lds_sum[t] = v.x;
     mega_lds_sum[256 + t] = v.y;
     mega_lds_sum[512 + t] = v.z;
 }
 #else
-__device__ __forceinline__ V3 lane_sum(const MegaLane &L) { return L.sum; }
-__device__ __forceinline__ void lane_sum_set(MegaLane &L, V3 v) { L.sum = v; }
+template <class ML>
+__device__ __forceinline__ V3 lane_sum(const ML &L) { return L.sum; }
+template <class ML>
+__device__ __forceinline__ void lane_sum_set(ML &L, V3 v) { L.sum = v; }
 #endif
 
 // The lane's RNG state (minstd word, normal cache) lives in LDS between its uses (sample
@@ -85,21 +93,25 @@ __device__ __forceinline__ void rng_word_unpack(uint32_t w, uint32_t &x, uint32_
 }
 #if defined(__HIPCC__)
 __shared__ uint32_t mega_lds_rng[2 * 256];
-__device__ __forceinline__ Rng lane_rng(const MegaLane &) {
+template <class ML>
+__device__ __forceinline__ Rng lane_rng(const ML &) {
     const int t = threadIdx.x;
     Rng r;
     rng_word_unpack(mega_lds_rng[t], r.x, r.saved_avail);
     r.saved = __uint_as_float(mega_lds_rng[256 + t]);
     return r;
 }
-__device__ __forceinline__ void lane_rng_set(MegaLane &, const Rng &r) {
+template <class ML>
+__device__ __forceinline__ void lane_rng_set(ML &, const Rng &r) {
     const int t = threadIdx.x;
     mega_lds_rng[t] = rng_word_pack(r.x, r.saved_avail);
     mega_lds_rng[256 + t] = __float_as_uint(r.saved);
 }
 #else
-__device__ __forceinline__ Rng lane_rng(const MegaLane &L) { return L.rng; }
-__device__ __forceinline__ void lane_rng_set(MegaLane &L, const Rng &r) { L.rng = r; }
+template <class ML>
+__device__ __forceinline__ Rng lane_rng(const ML &L) { return L.rng; }
+template <class ML>
+__device__ __forceinline__ void lane_rng_set(ML &L, const Rng &r) { L.rng = r; }
 #endif
 
 // The lane's sample counter, depth budget and recorded-vertex count, packed in one register
@@ -108,16 +120,18 @@ __device__ __forceinline__ void lane_rng_set(MegaLane &L, const Rng &r) { L.rng 
 struct LaneCtr {
     int s, power, nv;
 };
-__device__ __forceinline__ LaneCtr lane_ctr(const MegaLane &L) {
+template <class ML>
+__device__ __forceinline__ LaneCtr lane_ctr(const ML &L) {
     return LaneCtr{(int)(L.ctr & 0xfffffu), (int)((L.ctr >> 20) & 15u), (int)(L.ctr >> 24)};
 }
-__device__ __forceinline__ void lane_ctr_set(MegaLane &L, const LaneCtr &c) {
+template <class ML>
+__device__ __forceinline__ void lane_ctr_set(ML &L, const LaneCtr &c) {
     L.ctr = (uint32_t)c.s | (uint32_t)c.power << 20 | (uint32_t)c.nv << 24;
 }
 
 // Closest-hit query start for L.r: BVH::intersect's counters and root box (bvh.cpp:239-243).
-template <bool COUNT>
-__device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Counters &cnt) {
+template <bool COUNT, class ML>
+__device__ __forceinline__ void mega_begin(ML &L, const NodeRec &root, Counters &cnt) {
     float e;
     const bool hit = box_hit<false>(root.mn, root.mx, L.r, e);
     const uint32_t bits = (L.r.d.x > 0 ? 1u : 0u) | (L.r.d.y > 0 ? 2u : 0u) | (L.r.d.z > 0 ? 4u : 0u) | (hit ? 0u : 8u);
@@ -126,8 +140,8 @@ __device__ __forceinline__ void mega_begin(MegaLane &L, const NodeRec &root, Cou
 
 // Next sample of the lane's pixel: jittered camera ray (scene.cpp:36-39).  Fast mode: the
 // sample's own Philox-seeded stream (rt_path.h fast_sample_seed).
-template <bool COUNT, bool FAST = false>
-__device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
+template <bool COUNT, bool FAST = false, class ML>
+__device__ __forceinline__ void mega_sample(ML &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
                                             Counters &cnt) {
     LaneCtr c = lane_ctr(L);
     Rng rng = FAST ? Rng{fast_sample_seed(L.gpix, (uint32_t)c.s), 0u, 0.f} : lane_rng(L);
@@ -145,8 +159,8 @@ __device__ __forceinline__ void mega_sample(MegaLane &L, const DevScene &sc, con
 }
 
 // A new pixel: seed its RNG (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1), first sample.
-template <bool COUNT>
-__device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, const ShardGeom &g, int p,
+template <bool COUNT, class ML>
+__device__ __forceinline__ void mega_assign(ML &L, const DevScene &sc, const ShardGeom &g, int p,
                                             const NodeRec &root, Counters &cnt) {
     L.pix = p;
     lane_ctr_set(L, LaneCtr{0, 0, 0});
@@ -161,8 +175,8 @@ __device__ __forceinline__ void mega_assign(MegaLane &L, const DevScene &sc, con
 // Fast mode: queue item q = chunk * n_pixels + pixel (every pixel's first chunk, then the
 // second, ...: neighbouring lanes take neighbouring pixels); samples [chunk*cs, +cs) of the
 // pixel, partial sum to slot q of the chunk-major partial buffer.
-template <bool COUNT>
-__device__ __forceinline__ void mega_assign_fast(MegaLane &L, const DevScene &sc, const ShardGeom &g, long long q,
+template <bool COUNT, class ML>
+__device__ __forceinline__ void mega_assign_fast(ML &L, const DevScene &sc, const ShardGeom &g, long long q,
                                                  int cs, int spp, const NodeRec &root, Counters &cnt) {
     const long long c = q / g.n_pixels;
     const int p = (int)(q - c * g.n_pixels);
@@ -203,13 +217,14 @@ inline bool spec_hint_take() {
 
 // End of a runahead job's sample (speculative runahead, below): adds it and starts the next
 // sample on this lane when no other job of its pixel is in flight, else waits (M_DONE_NEW).
-__device__ void spec_job_end(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st, int spp,
+template <class ML>
+__device__ void spec_job_end(ML &L, const DevScene &sc, const ShardGeom &g, const WfState &st, int spp,
                              float *out, const NodeRec &root, V3 color, LaneCtr c);
 
 // `tail` (wave-uniform): the wave runs runahead jobs (spec_manage below); a job's path end
 // goes to spec_job_end instead of the pixel sum in the lane.
-template <bool COUNT, bool FAST = false, class Stack>
-__device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
+template <bool COUNT, bool FAST = false, class Stack, class ML>
+__device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
                                            Counters &cnt, bool tail = false) {
     LaneRec P{st.rec_ab, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
@@ -272,8 +287,8 @@ __device__ __forceinline__ void mega_shade(MegaLane &L, const DevScene &sc, cons
 // internal node pushes the children whose boxes the ray hits (right, then left: left is
 // visited first).  `dir_rec` holds the un-normalized sample direction (light_pdf's
 // `direction`).  Returns true when the stack is empty.
-template <bool COUNT, class Stack>
-__device__ __forceinline__ bool light_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk, Counters &cnt,
+template <bool COUNT, class Stack, class TS>
+__device__ __forceinline__ bool light_step(const DevScene &sc, const Ray &r, TS &T, Stack &stk, Counters &cnt,
                                            const float4 *dir_rec) {
     const uint32_t id = stk.get(--T.sp).x;
     const NodeRec nd = load_node(sc.light_node, id);
@@ -308,8 +323,8 @@ __device__ __forceinline__ bool light_step(const DevScene &sc, const Ray &r, Tra
 // Shading of the light-split kernel: a READY lane runs shade_pre and starts its light walk
 // (or, without lights, finishes the vertex); an LREADY lane finishes the vertex with the
 // walked pdf.  The rest is mega_shade's: bounce, or fold and next sample / pixel.
-template <bool COUNT, bool FAST, class Stack>
-__device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc, const ShardGeom &g,
+template <bool COUNT, bool FAST, class Stack, class ML>
+__device__ __forceinline__ void mega_shade_split(ML &L, const DevScene &sc, const ShardGeom &g,
                                                  const WfState &st, int spp, float *out, unsigned *cost,
                                                  const NodeRec &root, Stack &stk, Counters &cnt) {
     const long long slot = mega_slot();
@@ -387,8 +402,8 @@ __device__ __forceinline__ void mega_shade_split(MegaLane &L, const DevScene &sc
 
 // One iteration of a wave's main loop for one lane, given the wave's decision: shade the
 // READY lanes this iteration (shade_now), or step the traversing lanes.
-template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT = false>
-__device__ __forceinline__ void mega_iterate(MegaLane &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
+template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT = false, class ML>
+__device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
                                              const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt,
                                              bool tail = false) {
@@ -587,7 +602,8 @@ __device__ __forceinline__ void spec_convert(MegaLane &L, const SpecView &V, int
 }
 
 // Start job (record r, sample t, epoch e) on this lane from state Y.
-__device__ __forceinline__ void spec_start(MegaLane &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
+template <class ML>
+__device__ __forceinline__ void spec_start(ML &L, const DevScene &sc, const ShardGeom &g, const NodeRec &root,
                                            uint32_t pix, uint32_t t, const Rng &Y) {
     L.pix = (int)pix;
     lane_ctr_set(L, LaneCtr{(int)t, 0, 0});
@@ -603,7 +619,8 @@ __device__ __forceinline__ void spec_start(MegaLane &L, const DevScene &sc, cons
 // waits for the next pass with its colour in the lane's sum slot.  Only this lane holds a job
 // of the pixel in the first case, and passes never overlap a shading step, so the record
 // update is this lane's alone.
-__device__ __forceinline__ void spec_job_end(MegaLane &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
+template <class ML>
+__device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                              int spp, float *out, const NodeRec &root, V3 color, LaneCtr c) {
     const int lane = (int)(mega_slot() & 63);
     const SpecView V{(uint4 *)st.mid, st.lanes, mega_slot() - lane};

@@ -300,16 +300,32 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
 #define RT_LEAF_N 2
 #endif
 
-// Resumable traversal state of one ray.
+// Resumable traversal state of one ray.  Two layouts: TravState keeps the node fields and
+// the leaf range in four registers; TravStateU shares two registers between them (a node
+// step never reads k / kend, a leaf step never reads a / b), so a traversing lane holds two
+// registers fewer through another lane's shading pass.  The lane-resident kernel uses
+// TravStateU: 53 -> 50 spilled VGPRs, 1145 -> 1132 ms (r03s5).  The runahead kernel keeps
+// TravState: with the shared layout its 8-way shards measured 0.8% slower (205 vs 203 ms mean).
 enum TravPhase : int { TP_NODE = 0, TP_LEAF = 1, TP_POP = 2 };
-struct TravState {
-    uint32_t a, b;   // TP_NODE: internal node being entered (b = split axis, a = left child)
+template <bool SHARED> struct TravFields;
+template <> struct TravFields<false> {
+    uint32_t a, b;      // TP_NODE: internal node being entered (b = split axis, a = left child)
     uint32_t k, kend;   // TP_LEAF: triangles still to test
+};
+template <> struct TravFields<true> {
+    union { uint32_t a; uint32_t k; };      // TP_NODE: left child / TP_LEAF: next triangle
+    union { uint32_t b; uint32_t kend; };   // TP_NODE: split axis / TP_LEAF: end of the leaf's range
+};
+template <bool SHARED>
+struct TravStateT : TravFields<SHARED> {
+    static constexpr bool kShared = SHARED;
     float acc;       // best t inside the subtree being traversed (the reference's local best)
     int sp;
     int phase;
     Hit best;        // global winner so far (strict <, first of equal t wins)
 };
+using TravState = TravStateT<false>;
+using TravStateU = TravStateT<true>;
 
 // Where trav_step reads child pairs from: the breadth-first node array in HBM.
 struct GlobalNodes {
@@ -329,19 +345,27 @@ struct ArrayStack {
 
 // Enter a node given its (a, b) fields: internal -> TP_NODE, leaf -> TP_LEAF (an empty
 // leaf returns at once).
-__device__ __forceinline__ void trav_enter(TravState &T, uint32_t a, uint32_t b) {
-    T.a = a;
-    T.b = b;
-    T.k = a;
-    T.kend = a + (b >> 2);
-    T.phase = b < 3u ? TP_NODE : (T.kend > T.k ? TP_LEAF : TP_POP);
+template <class TS>
+__device__ __forceinline__ void trav_enter(TS &T, uint32_t a, uint32_t b) {
+    if constexpr (TS::kShared) {
+        const bool node = b < 3u;
+        T.a = a;                            // = T.k
+        T.b = node ? b : a + (b >> 2);      // = T.kend for a leaf
+        T.phase = node ? TP_NODE : ((b >> 2) != 0u ? TP_LEAF : TP_POP);
+    } else {
+        T.a = a;
+        T.b = b;
+        T.k = a;
+        T.kend = a + (b >> 2);
+        T.phase = b < 3u ? TP_NODE : (T.kend > T.k ? TP_LEAF : TP_POP);
+    }
 }
 
 // BVH::intersect entry (bvh.cpp:239-243) for a queued ray: counters, and the root box
 // result the producer stored (bits from load_qray_trav).  False = the ray misses the scene
 // (T.best says so).  (root_a, root_b) are the root node's fields.
-template <bool COUNT>
-__device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint32_t root_b, TravState &T,
+template <bool COUNT, class TS>
+__device__ __forceinline__ bool trav_start(uint32_t bits, uint32_t root_a, uint32_t root_b, TS &T,
                                            Counters &cnt) {
     if (COUNT) { cnt.rays++; cnt.aabb++; }
     T.best.t = 1e9f;
@@ -364,8 +388,8 @@ constexpr int kMaxPops = RT_MAX_POPS;
 // The return of trav_step: merge subtree bests upwards until a far child is to be visited
 // (enter it: false), the stack is empty (T.best is final: true) or kMaxPops frames are
 // popped (false, still TP_POP).
-template <class Stack>
-__device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
+template <class Stack, class TS>
+__device__ __forceinline__ bool trav_pop(TS &T, Stack &stk) {
     float acc = T.acc;
     int sp = T.sp;
     for (int n = 0;; ++n) {
@@ -401,8 +425,8 @@ __device__ __forceinline__ bool trav_pop(TravState &T, Stack &stk) {
 // The node part of a traversal step: the child pair q[0..3] (two 32-B node records) of the
 // internal node T is entering; pushes the far child when both are hit, enters the near one
 // (or the far one alone, or returns: T.phase = TP_POP).
-template <bool COUNT, class Stack>
-__device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravState &T, Stack &stk, Counters &cnt) {
+template <bool COUNT, class Stack, class TS>
+__device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TS &T, Stack &stk, Counters &cnt) {
     NodeRec L, R;
     L.mn[0] = q[0].x; L.mn[1] = q[0].y; L.mn[2] = q[0].z; L.mx[0] = q[0].w; L.mx[1] = q[1].x; L.mx[2] = q[1].y;
     L.a = __float_as_uint(q[1].z); L.b = __float_as_uint(q[1].w);
@@ -442,8 +466,8 @@ __device__ __forceinline__ void node_step(const float4 q[4], const Ray &r, TravS
 // Both memory reads of the step issue before either test (node lanes and leaf lanes load
 // through the same registers), so a wave split between node and leaf steps waits for one
 // round trip per iteration, not two.
-template <bool COUNT, class Stack, class Nodes>
-__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
+template <bool COUNT, class Stack, class Nodes, class TS>
+__device__ __forceinline__ bool trav_step(const DevScene &sc, const Ray &r, TS &T, Stack &stk,
                                           const Nodes &nodes, Counters &cnt) {
     constexpr int N = RT_LEAF_N;
     const bool at_node = T.phase == TP_NODE, at_leaf = T.phase == TP_LEAF;
@@ -575,8 +599,8 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
 // round per step).  A wave mostly at leaves (a scene of a few dozen triangles, whose tree
 // is a few levels deep) otherwise serves kCoopLeaves of its leaf lanes per step and idles
 // the rest (rt_device.hip kCoopRoundMin*).
-template <bool COUNT, int kCoopLeaves, class Stack, class Nodes>
-__device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TravState &T, Stack &stk,
+template <bool COUNT, int kCoopLeaves, class Stack, class Nodes, class TS>
+__device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TS &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active, int round_min) {
     static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
     __shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)

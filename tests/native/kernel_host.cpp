@@ -5,6 +5,7 @@
 #include <cstring>
 #include <vector>
 #include <algorithm>
+#include <type_traits>
 #include "../../raytracing-hw_amd/csrc/rt_mega.h"
 #include "../../raytracing-hw_amd/csrc/rt_bvh_layout.h"
 #include "../../include/rt_hw.h"
@@ -186,7 +187,9 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     st.mid = mid.data();
     const rtd::NodeRec root = rtd::load_node(rtd::mega_nodes(sc), 0);
     const rtd::GlobalNodes nodes{sc.node};
-    std::vector<rtd::MegaLane> lanes((size_t)waves * 64);
+    // lane state as in rt_device.hip: TravState for the runahead kernel, TravStateU otherwise
+    using Lane = std::conditional_t<SPEC, rtd::MegaLane, rtd::MegaLaneU>;
+    std::vector<Lane> lanes((size_t)waves * 64);
     std::vector<std::vector<uint2>> stacks((size_t)waves * 64, std::vector<uint2>(rtd::kStack));
     for (auto &L : lanes) { L.pix = -1; L.state = rtd::M_IDLE; }
     std::vector<char> exhausted(waves, 0), done(waves, 0), tail(waves, 0), wave_room(waves, 0);
@@ -198,7 +201,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
         ++g_rounds;
         for (int w = 0; w < waves; ++w) {
             if (done[w]) continue;
-            rtd::MegaLane *W = &lanes[(size_t)w * 64];
+            Lane *W = &lanes[(size_t)w * 64];
             if (!exhausted[w] && g_static_per_wave > 0) {   // static allotment: wave w renders items [w*P, w*P+P)
                 for (int l = 0; l < 64 && l < g_static_per_wave; ++l) {
                     const long long p = (long long)w * g_static_per_wave + l;
@@ -221,7 +224,8 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                     if (base + cm >= n) exhausted[w] = 1;
                 }
             }
-            if (SPEC && exhausted[w] && !tail[w]) {
+            if constexpr (SPEC) {
+            if (exhausted[w] && !tail[w]) {
                 const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
                 for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], V, l);
                 rtd::g_mega_slot = (long long)w * 64;
@@ -243,6 +247,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                                                     rtd::SpecView{(uint4 *)st.mid, st.lanes, (long long)w * 64}, spp,
                                                     out, root);
                 }
+            }
             }
             bool any = false;
             int nr = 0, nt = 0;
