@@ -56,7 +56,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_AABB, B_TRI, B_SHADE = 24, 36, 156
 B_RAY_IO = 24 + 4 + 16     # wf_extend per ray: ray (6 floats) + queue slot in, hit (t, u, v, prim) out
-PROFILE_PREFIX = "r03u"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
+PROFILE_PREFIX = "r03w"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
 
 
 def import_pkg():
