@@ -34,8 +34,11 @@ cpu_baseline: the reference itself (oracle/_ref/ref_render, built from /root/ref
            absent.
 roofline.bound follows the committed counters: "latency/issue" when the HBM-side traffic
            is under half the algorithmic model's or below the VALU issue utilisation
-           (roofline.issue: VALU instructions per SIMD-cycle from the SQ passes, lane
-           utilisation, SALU share, wait share), else "hbm".
+           (roofline.issue: VALU instructions per SIMD-cycle from the SQ passes against the
+           SIMD-32 ceiling of 0.5, lane utilisation, SALU share, wait share), else "hbm";
+           "unmeasured" when no PMC pass of the command is committed.  --gpus N reads rank 0's
+           shard passes (profiles/<SHARD_PROFILE_PREFIX>_shard_*_w<N>.csv, tools/pmc_shard.sh)
+           for the kernel that rendered it (the runahead instantiation at 4 and 8 ways).
 frame_matches_reference: the 8-bit frame's sha1 against the reference's own finished frame of
            the same workload (tests/golden/golden_meta.json "frames"), computed after the timed
            region.
@@ -57,6 +60,18 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_AABB, B_TRI, B_SHADE = 24, 36, 156
 B_RAY_IO = 24 + 4 + 16     # wf_extend per ray: ray (6 floats) + queue slot in, hit (t, u, v, prim) out
 PROFILE_PREFIX = "r03w"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
+# profiles/<prefix>_shard_{fetch,write,sq1,sq2}_w<N>.csv: rank 0's shard of the N-way split
+# (tools/pmc_shard.sh), the counters of an --gpus N line
+SHARD_PROFILE_PREFIX = "r04"
+# rocprofv3 names of the two parity instantiations of the default kernel: the plain one (one
+# GPU) and the runahead one (shards of at most 2 pixels per lane: the 4- and 8-way splits)
+KERNEL_PLAIN = "void rt_mega_kernel<false, false, false, false>"
+KERNEL_SPEC = "void rt_mega_kernel<false, false, false, true>"
+
+
+def pmc_file(prefix, kind, world):
+    """The committed PMC summary of pass `kind` for this world size."""
+    return f"{prefix}_{kind}_1080p256.csv" if world == 1 else f"{prefix}_shard_{kind}_w{world}.csv"
 
 
 def import_pkg():
@@ -123,16 +138,15 @@ def cpu_baseline(scene_path, width, height, spp, rows, stride, threads):
             "sample": sample + " (oracle/rt_oracle.cpp restatement)", "seconds": secs}
 
 
-def pmc_mean(path, counter, kernel_prefix, duration=False):
-    """Mean per dispatch of `counter` for the parity launch of `kernel_prefix` in a rocprofv3
-    --stats PMC summary (None when absent); with duration=True, that pass's average dispatch
-    duration in seconds instead.  The fast-mode instantiation ends its template list in
-    "true>" and is skipped."""
+def pmc_mean(path, counter, kname, duration=False):
+    """Mean per dispatch of `counter` for the launch of kernel `kname` (its full template list,
+    KERNEL_PLAIN or KERNEL_SPEC) in a rocprofv3 --stats PMC summary (None when absent); with
+    duration=True, that pass's average dispatch duration in seconds instead."""
     import csv
     if not os.path.exists(path):
         return None
     for row in csv.reader(open(path)):
-        if row and row[0].startswith(kernel_prefix) and "true>(" not in row[0] and row[1] == counter:
+        if row and row[0].startswith(kname + "(") and row[1] == counter:
             return float(row[5]) * 1e-9 if duration else float(row[4])
     return None
 
@@ -141,27 +155,32 @@ SIMDS = 256 * 4            # MI355X: 256 CUs x 4 SIMD-32
 NOMINAL_CLOCK_HZ = 2.4e9   # used only when no GRBM_GUI_ACTIVE pass is committed
 
 
-def pmc_issue(prefix, kernel_prefix):
-    """Issue-side picture of the launch from the committed SQ passes (tools/profile.sh):
-    VALU wave-instructions per SIMD per cycle over the pass's own dispatch duration (a SIMD-32
-    issues a wave64 VALU instruction in 2 cycles, so 0.5 is its ceiling), the VALU lane
-    utilisation and the wait share."""
-    sq1, sq2 = prefix + "_sq1_1080p256.csv", prefix + "_sq2_1080p256.csv"
-    valu = pmc_mean(sq2, "SQ_INSTS_VALU", kernel_prefix)
-    salu = pmc_mean(sq2, "SQ_INSTS_SALU", kernel_prefix)
-    tcv = pmc_mean(sq1, "SQ_THREAD_CYCLES_VALU", kernel_prefix)
-    aiv = pmc_mean(sq1, "SQ_ACTIVE_INST_VALU", kernel_prefix)
-    wait = pmc_mean(sq1, "SQ_WAIT_ANY", kernel_prefix)
-    wcyc = pmc_mean(sq1, "SQ_WAVE_CYCLES", kernel_prefix)
-    grbm = pmc_mean(sq1, "GRBM_GUI_ACTIVE", kernel_prefix)
-    avg_s = pmc_mean(sq2, "SQ_INSTS_VALU", kernel_prefix, duration=True)
+# VALU issue ceiling of one SIMD: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+# (MI355X_MICROARCH.md, "Wave scheduling" and the constants row "v_fma_f32 (wave64) 2 cyc
+# (SIMD-32)"), so at most 0.5 wave-instructions issue per SIMD per cycle.
+VALU_ISSUE_CEILING = 0.5
+
+
+def pmc_issue(prefix, kname, world=1):
+    """Issue-side picture of the launch from the committed SQ passes (tools/profile.sh,
+    tools/pmc_shard.sh): VALU wave-instructions per SIMD per cycle over the pass's own dispatch
+    duration and its share of VALU_ISSUE_CEILING, the VALU lane utilisation and the wait share."""
+    sq1, sq2 = pmc_file(prefix, "sq1", world), pmc_file(prefix, "sq2", world)
+    valu = pmc_mean(sq2, "SQ_INSTS_VALU", kname)
+    salu = pmc_mean(sq2, "SQ_INSTS_SALU", kname)
+    tcv = pmc_mean(sq1, "SQ_THREAD_CYCLES_VALU", kname)
+    aiv = pmc_mean(sq1, "SQ_ACTIVE_INST_VALU", kname)
+    wait = pmc_mean(sq1, "SQ_WAIT_ANY", kname)
+    wcyc = pmc_mean(sq1, "SQ_WAVE_CYCLES", kname)
+    grbm = pmc_mean(sq1, "GRBM_GUI_ACTIVE", kname)
+    avg_s = pmc_mean(sq2, "SQ_INSTS_VALU", kname, duration=True)
     if valu is None or not avg_s:
         return None
     clock = grbm / 8.0 / avg_s if grbm else NOMINAL_CLOCK_HZ
     per_simd_cycle = valu / (SIMDS * avg_s * clock)
     return {"valu_inst_per_simd_cycle": round(per_simd_cycle, 4),
-            "issue_frac": round(per_simd_cycle / 1.0, 4),
-            "issue_frac_of_simd32_peak": round(per_simd_cycle / 0.5, 4),
+            "issue_frac_of_simd32_peak": round(per_simd_cycle / VALU_ISSUE_CEILING, 4),
+            "issue_ceiling": "0.5 wave64 VALU instructions per SIMD-32 per cycle (MI355X_MICROARCH.md, Wave scheduling)",
             "lane_util": None if not (tcv and aiv) else round(tcv / (aiv * 64.0), 4),
             "salu_per_valu": None if salu is None else round(salu / valu, 4),
             "wait_any_frac": None if not (wait and wcyc) else round(wait / wcyc, 4),
@@ -183,20 +202,13 @@ def reference_frame_sha1(scene, W, H, S):
     return None
 
 
-def pmc_traffic(fetch_csv, write_csv, kernel_prefix):
-    """HBM-side bytes per launch of `kernel_prefix` from rocprofv3 PMC summaries
-    (tools/profile.sh, separate --pmc passes of the same command): FETCH_SIZE doubled (the
-    gfx950 correction of MI355X_MICROARCH.md, HBM section; FETCH_SIZE counts half of the
-    bytes of 16-B-per-lane reads) plus WRITE_SIZE, both KiB per dispatch."""
-    import csv
-    def mean(path, counter):
-        for row in csv.reader(open(path)):
-            # the parity launch only (the fast-mode instantiation ends its template list in "true>")
-            if row and row[0].startswith(kernel_prefix) and "true>(" not in row[0] and row[1] == counter:
-                return float(row[4]) * 1024.0
-        return None
-    f, w = mean(fetch_csv, "FETCH_SIZE"), mean(write_csv, "WRITE_SIZE")
-    return None if f is None or w is None else (2.0 * f + w, f + w)
+def pmc_traffic(fetch_csv, write_csv, kname):
+    """HBM-side bytes per launch of kernel `kname` from rocprofv3 PMC summaries
+    (tools/profile.sh, tools/pmc_shard.sh: separate --pmc passes of the same workload):
+    FETCH_SIZE doubled (the gfx950 correction of MI355X_MICROARCH.md, HBM section; FETCH_SIZE
+    counts half of the bytes of 16-B-per-lane reads) plus WRITE_SIZE, both KiB per dispatch."""
+    f, w = pmc_mean(fetch_csv, "FETCH_SIZE", kname), pmc_mean(write_csv, "WRITE_SIZE", kname)
+    return None if f is None or w is None else (2.0 * f * 1024.0 + w * 1024.0, f * 1024.0 + w * 1024.0)
 
 
 def main():
@@ -314,7 +326,7 @@ def main():
             counts = st
     torch.cuda.synchronize()
 
-    kernel_ms, ext_ms, ext_n, ext_rays, order_ms = [], [], [], [], []
+    kernel_ms, ext_ms, ext_n, ext_rays, order_ms, sched = [], [], [], [], [], 0
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -325,6 +337,7 @@ def main():
         ext_ms.append(st["extend_ms"])
         ext_n.append(st["extend_launches"])
         ext_rays.append(st["extend_rays"])
+        sched |= st["schedule"]
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -387,34 +400,33 @@ def main():
             avg_s = float(np.sum(ext_ms)) / float(np.sum(ext_n)) / 1e3
             kname = "wf_extend_kernel"
         else:
-            # one launch renders the frame: the whole-path model over the launch time
+            # one launch renders the frame (rank 0's shard): the whole-path model over the launch time
             bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
-            kname = "rt_mega_kernel"
+            kname = KERNEL_SPEC if sched & rt.SCHED_RUNAHEAD else KERNEL_PLAIN
         achieved = bytes_launch / avg_s / 1e9
         traffic, traffic_u, traffic_src, issue = None, None, None, None
         if args.traffic_from != "none":
             prefix = args.traffic_from
-            default_cfg = (args.scene, W, H, S, args.kernel, world) == ("sponza", 1920, 1080, 256, 0, 1)
+            default_cfg = (args.scene, W, H, S, args.kernel) == ("sponza", 1920, 1080, 256, 0)
             if prefix == "auto":
-                prefix = os.path.join(ROOT, "profiles", PROFILE_PREFIX) if default_cfg else None
+                prefix = os.path.join(ROOT, "profiles", PROFILE_PREFIX if world == 1 else SHARD_PROFILE_PREFIX) \
+                    if default_cfg else None
             if prefix:
-                fc, wc = prefix + "_fetch_1080p256.csv", prefix + "_write_1080p256.csv"
+                fc, wc = pmc_file(prefix, "fetch", world), pmc_file(prefix, "write", world)
                 if os.path.exists(fc) and os.path.exists(wc):
-                    t = pmc_traffic(fc, wc, "void " + kname + "<false")
+                    t = pmc_traffic(fc, wc, kname)
                     if t is not None:
                         traffic, traffic_u = t[0] / launches, t[1] / launches
                         traffic_src = os.path.relpath(fc, ROOT) + " + " + os.path.relpath(wc, ROOT)
-                issue = pmc_issue(prefix, "void " + kname + "<false")
+                issue = pmc_issue(prefix, kname, world)
         frac = achieved / HBM_PEAK_GBS
         traffic_frac = None if traffic is None else traffic / avg_s / 1e9 / HBM_PEAK_GBS
-        # the label follows the counters: HBM-bound only when the measured HBM-side traffic is
-        # at least half of what the algorithmic model asks for
         # the label follows the counters: HBM-bound only when the measured
         # HBM-side traffic is at least half of what the algorithmic model asks for and the
-        # memory side is busier than the issue side (VALU issue rate / the SIMD-32 ceiling)
+        # memory side is busier than the issue side (VALU issue rate / VALU_ISSUE_CEILING)
         issue_share = None if issue is None else issue["issue_frac_of_simd32_peak"]
         if traffic_frac is None:
-            bound = "hbm (algorithmic model only: no PMC pass)"
+            bound = "unmeasured (no PMC pass committed for this command)"
         elif traffic_frac < 0.5 * frac or (issue_share is not None and issue_share > traffic_frac):
             bound = "latency/issue"
         else:
@@ -454,7 +466,6 @@ def main():
                          "traffic_undoubled": None if traffic_u is None else int(traffic_u),
                          "traffic_frac": None if traffic_frac is None else round(traffic_frac, 4),
                          "issue": issue,
-                         "issue_frac": None if issue is None else issue["issue_frac"],
                          "traffic_source": traffic_src,
                          "kernel": kname, "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
                          "launches_per_frame": launches,

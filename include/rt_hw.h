@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum rt_status {
     RT_OK = 0,
@@ -129,6 +129,10 @@ typedef struct {
  * runahead): same bits, shorter frame tail.  This flag turns it off.  (Counting renders,
  * count = 1, never use it: their counters are those of the sequential chain.) */
 #define RT_FLAG_NO_RUNAHEAD 16
+/* Path-pool schedule (rt_pool.h; parity mode, shards of more than 2 pixels per lane): each
+ * wave keeps 64 x 2 paths in HBM and its lanes traverse whichever path is queued, so no lane
+ * waits for a shading batch.  Same bits. */
+#define RT_FLAG_POOL 64
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */
@@ -150,7 +154,17 @@ typedef struct {
     double gather_ms;       /* rt_render_frame / _multi: device-to-device copies of the slowest
                                device + assembly on the root device + the copy to the host  */
     uint64_t devices;       /* devices that rendered                                       */
+    uint64_t schedule;      /* RT_SCHED_* bits of the kernels that rendered (ABI 5; for
+                               rt_render_frame / _multi the union over the shards)          */
 } rt_stats;
+
+/* rt_stats.schedule bits: which instantiation of the sample loop ran */
+#define RT_SCHED_LANE 1         /* lane-resident kernel (rt_mega.h), no runahead            */
+#define RT_SCHED_RUNAHEAD 2     /* lane-resident kernel with speculative sample runahead    */
+#define RT_SCHED_FAST 4         /* fast mode (RT_FLAG_FAST)                                 */
+#define RT_SCHED_LIGHT_SPLIT 8  /* light-split kernel (RT_FLAG_LIGHT_SPLIT)                 */
+#define RT_SCHED_WAVEFRONT 16   /* wavefront launches (RT_KERNEL_WAVEFRONT)                 */
+#define RT_SCHED_POOL 32        /* path-pool schedule of the lane-resident kernel (rt_pool.h) */
 
 /* --- scene ------------------------------------------------------------------------ */
 int rt_scene_load_gltf(const char *path, int32_t width, int32_t height, int32_t samples, rt_scene **out);
@@ -217,7 +231,10 @@ int rt_device_synchronize(void);
  * (rt_wavefront.h rcp_ieee) against IEEE division over every float with a normal
  * reciprocal; which 1: the computed linear texel decode (rt_path.h unorm8) against
  * (float)b / 255.f for every byte, and the packed LDS RNG word round trip over every minstd
- * state; *mismatches = values that differ (0 = exact). */
+ * state and both normal-cache flags; which 2: the cooperative leaf step (rt_wavefront.h
+ * trav_step_coop) against the per-lane in-order strict-< loop over 2^16 synthetic leaves rich
+ * in equal-t ties, NaN and infinite vertices (four launches); *mismatches = values (cases)
+ * that differ (0 = exact). */
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches);
 
 #ifdef __cplusplus

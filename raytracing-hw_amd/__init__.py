@@ -44,7 +44,7 @@ class RtSceneView(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 4          # include/rt_hw.h RT_ABI_VERSION
+ABI_VERSION = 5          # include/rt_hw.h RT_ABI_VERSION
 KERNEL_LANE = 0          # RT_KERNEL_LANE: lane-resident persistent kernel (default)
 KERNEL_WAVEFRONT = 4     # RT_KERNEL_WAVEFRONT: init / extend / shade launches
 FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES
@@ -53,6 +53,9 @@ FLAG_LIGHT_SPLIT = 4     # RT_FLAG_LIGHT_SPLIT: light-pdf walk as its own traver
 FLAG_NATURAL_ORDER = 8   # RT_FLAG_NATURAL_ORDER: row-major pixel order instead of the in-frame heaviest-first order
 FLAG_NO_RUNAHEAD = 16    # RT_FLAG_NO_RUNAHEAD: no speculative sample runahead in the waves' tails (same bits)
 FLAG_HEAVY_ORDER = 32    # RT_FLAG_HEAVY_ORDER: the heaviest-first order below 128 spp too (same bits)
+# RtStats.schedule bits (include/rt_hw.h RT_SCHED_*): the kernels that rendered
+SCHED_LANE, SCHED_RUNAHEAD, SCHED_FAST, SCHED_LIGHT_SPLIT, SCHED_WAVEFRONT, SCHED_POOL = 1, 2, 4, 8, 16, 32
+FLAG_POOL = 64           # RT_FLAG_POOL: path-pool schedule (rt_pool.h; same bits)
 
 
 class RtParams(ctypes.Structure):
@@ -67,7 +70,8 @@ class RtStats(ctypes.Structure):
                 ("light_aabb_tests", ctypes.c_uint64), ("light_tri_tests", ctypes.c_uint64), ("shading_hits", ctypes.c_uint64),
                 ("render_ms", ctypes.c_double), ("extend_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
                 ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64), ("extend_rays", ctypes.c_uint64),
-                ("order_ms", ctypes.c_double), ("gather_ms", ctypes.c_double), ("devices", ctypes.c_uint64)]
+                ("order_ms", ctypes.c_double), ("gather_ms", ctypes.c_double), ("devices", ctypes.c_uint64),
+                ("schedule", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -216,14 +220,15 @@ class Scene:
         _check(lib().rt_scene_upload(self._h, device))
 
     def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False, fast=False, fast_chunk=0,
-                device=0, light_split=False, natural_order=False, runahead=True, heavy_order=False):
+                device=0, light_split=False, natural_order=False, runahead=True, heavy_order=False, pool=False):
         flags = ((FLAG_KERNEL_TIMES if kernel_times else 0) | (FLAG_FAST if fast else 0) |
                  (FLAG_LIGHT_SPLIT if light_split else 0) | (FLAG_NATURAL_ORDER if natural_order else 0) |
-                 (0 if runahead else FLAG_NO_RUNAHEAD) | (FLAG_HEAVY_ORDER if heavy_order else 0))
+                 (0 if runahead else FLAG_NO_RUNAHEAD) | (FLAG_HEAVY_ORDER if heavy_order else 0) |
+                 (FLAG_POOL if pool else 0))
         return RtParams(spp or 0, rank, world, row_block, int(count), kernel, flags, fast_chunk, device)
 
     def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0, fast=False,
-                    fast_chunk=0, light_split=False, natural_order=False, runahead=True, heavy_order=False):
+                    fast_chunk=0, light_split=False, natural_order=False, runahead=True, heavy_order=False, pool=False):
         """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42).
         fast=True: fast mode (RT_FLAG_FAST, work units of fast_chunk samples): statistically
         equivalent to the reference, not bit-identical.  light_split / natural_order /
@@ -234,7 +239,7 @@ class Scene:
         st = RtStats()
         p = self._params(spp, rank, world, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk, device=device,
                          light_split=light_split, natural_order=natural_order, runahead=runahead,
-                         heavy_order=heavy_order)
+                         heavy_order=heavy_order, pool=pool)
         _check(lib().rt_render(self._h, ctypes.byref(p), out.ctypes.data_as(_c_f), ctypes.byref(st)))
         return out, st.as_dict()
 
@@ -271,12 +276,12 @@ class Scene:
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
                       kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0, device=0,
-                      light_split=False, natural_order=False, runahead=True, heavy_order=False):
+                      light_split=False, natural_order=False, runahead=True, heavy_order=False, pool=False):
         """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream, on
         `device` (upload(device) first).  kernel_times: per-launch HIP-event timing of the
         wavefront kernels (needs stats).  fast: fast mode (RT_FLAG_FAST), see render_sums."""
         p = self._params(spp, rank, world, row_block, count, kernel, kernel_times, fast, fast_chunk, device,
-                         light_split, natural_order, runahead, heavy_order)
+                         light_split, natural_order, runahead, heavy_order, pool)
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))

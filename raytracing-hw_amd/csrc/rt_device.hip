@@ -32,6 +32,7 @@
 #include "rt_wavefront.h"
 #include <type_traits>
 #include "rt_mega.h"
+#include "rt_pool.h"
 #include "rt_quant_lut.h"
 #include "rt_scene.h"
 #include "rt_bvh_layout.h"
@@ -46,9 +47,9 @@ using rtd::shard_row;
 #define RT_MEGA_WPE 5
 #endif
 constexpr int kMegaWpe = RT_MEGA_WPE;   // waves per SIMD the register allocation targets (96 VGPRs)
-// The runahead instantiation runs shards of at most one pixel per lane, which the
-// five-wave grid does not fill anyway (an 8-way shard of the headline: 1013 blocks, 4
-// waves per SIMD): 128 VGPRs instead of 96 keep its management pass from spilling the loop.
+// The runahead instantiation runs shards of at most kSpecPixelsPerLane (2) pixels per lane
+// (an 8-way shard of the headline: 1013 blocks, 4 waves per SIMD, one pixel per lane; a
+// 4-way shard two): 128 VGPRs instead of 96 keep its management pass from spilling the loop.
 #ifndef RT_SPEC_WPE
 #define RT_SPEC_WPE 4
 #endif
@@ -65,7 +66,7 @@ constexpr int kMegaWpeSpec = RT_SPEC_WPE;
 #define RT_SPEC_SHADE_MIN 40
 #endif
 constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
-constexpr int kShadeMin = RT_SHADE_MIN;
+constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
 // Traversal iterations between two shading passes run as an inner loop of their own (no pixel
 // claim, runahead pass or schedule decision per iteration).  0: one iteration per pass of the
 // main loop (round 2), for A/B builds.
@@ -96,7 +97,7 @@ constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
 #ifndef RT_SPEC_COOP_LEAVES
 #define RT_SPEC_COOP_LEAVES 16
 #endif
-constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // a wave shades once this many lanes are READY (or none traverses)
+constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // the runahead kernel's coop leaf records per wave
 // Leaf rounds per coop step (rt_wavefront.h trav_step_coop round_min): a further round
 // while at least this many leaf lanes are unserved.  Plain kernel: 8 (sponza 1080p 1292 ->
 // 1278 ms against one round per step).  Runahead kernel: 4 on scenes of fewer than
@@ -184,6 +185,17 @@ struct rt_device_scene {
     // pixel order of the current render (heaviest first, spread; see launch_order)
     void *order_buf = nullptr;
     size_t order_bytes = 0;
+    // rt_render_frame, kept between frames: the device's render and copy streams, two shard
+    // buffers (float sums then 8-bit rows) and the events that order their reuse; on the root
+    // device also the staging / frame buffers and the row map (FrameRoot)
+    hipStream_t fr_stream = nullptr, cp_stream = nullptr;
+    void *fr_buf[2] = {nullptr, nullptr};
+    size_t fr_bytes[2] = {0, 0};
+    hipEvent_t fr_copied[2] = {nullptr, nullptr};   // copy of buffer b done (reuse after it)
+    hipEvent_t fr_finished = nullptr;               // shard finished to 8 bits (copy may start)
+    hipEvent_t fr_last = nullptr;                   // the device's last copy of the frame done
+    void *root_buf = nullptr;
+    size_t root_bytes = 0;
 };
 
 #define HIP_TRY(expr)                                                                          \
@@ -445,6 +457,137 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     __syncthreads();
     if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
 #endif
+    rtd::counters_flush<COUNT>(cnt, counters);
+}
+
+// ------------------------------------------------------------------------ path pool (rt_pool.h)
+// The lane-resident path tracer with the wave's paths in a pool: lanes are traversal slots fed
+// from the wave's traversal queue, ready paths are shaded kPoolBatch at a time by lanes 0..n-1.
+// Parity mode, shards of more than kSpecPixelsPerLane pixels per lane (the 1- and 2-GPU
+// frames).  Exit: every path of the pool retires once the pixel queue is empty (it is then in
+// no ring and no lane), and the loop ends when no lane traverses and both rings are empty.
+// RT_POOL_PARK: the traversal state of the lanes is parked in memory around a shading pass
+// (0: kept in registers, spilled where the compiler decides).
+#ifndef RT_POOL_PARK
+#define RT_POOL_PARK 1
+#endif
+constexpr bool kPoolPark = RT_POOL_PARK != 0;
+template <bool COUNT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMegaWpe, 8)))
+rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
+               unsigned long long *queue, const int *order) {
+    const long long n_items = g.n_pixels;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ float lut[256];
+    __shared__ uint8_t ring_q[4][rtd::kPool], ring_r[4][rtd::kPool];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) lut[k] = sc_in.lut[k];
+    __syncthreads();
+    DevScene sc = sc_in;
+    sc.lut = lut;
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    uint2 spill[rtd::kStack - rtd::kLdsStack];
+    rtd::LdsStackT<rtd::kLdsStack> S{spill};
+    const rtd::GlobalNodes nodes{sc.node};
+    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
+    const rtd::PoolPlanes V{st.mid, st.lanes};
+    const long long wbase = ((long long)blockIdx.x * 4 + wave) * rtd::kPool;   // the wave's first path id
+    uint8_t *rq = ring_q[wave], *rr = ring_r[wave];
+    int qh = 0, qt = 0, rh = 0, rt = 0;   // ring heads / tails (running counts, wave-uniform)
+    bool exhausted = false;
+    for (int q = 0; q < rtd::kPoolPerLane; ++q) {   // every path of the pool takes a pixel
+        const int j = lane + 64 * q;
+        const int pix = rtd::pool_claim(true, queue, n_items, order, exhausted);
+        if (pix >= 0) rtd::pool_assign(V, wbase + j, sc, g, pix, root);
+        rtd::pool_push(rq, qt, pix >= 0, j);
+    }
+    rtd::Ray r;
+    rtd::TravStateU T;
+    int jc = 0;          // the path this lane traverses (number in the pool)
+    bool trav = false;
+    // a traversal that has ended (done): its hit to the path record, the path to the ready ring
+    auto finish = [&](bool done) {
+        if (done) *V.C(wbase + jc) = make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
+        rtd::pool_push(rr, rt, done, jc);
+    };
+    // free lanes take queued paths (ring order)
+    auto refill = [&]() {
+        const unsigned long long fm = __ballot(!trav);
+        const int nq = qt - qh, nf = __popcll(fm);
+        const int take = nf < nq ? nf : nq;
+        if (take <= 0) return;
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+        bool done = false;
+        if (!trav && rank < take) {
+            jc = rq[(unsigned)(qh + rank) % (unsigned)rtd::kPool];
+            uint32_t miss;
+            r = rtd::pool_load_ray(V, wbase + jc, miss);
+            trav = rtd::trav_start<COUNT>(miss ? 8u : 0u, root.a, root.b, T, cnt);
+            done = !trav;   // the ray misses the scene box: no hit
+        }
+        qh += take;
+        finish(done);
+    };
+    for (;;) {
+        refill();
+        const int nt = __popcll(__ballot(trav)), nready = rt - rh;
+        if (nt == 0 && nready == 0) break;   // (the refill emptied the queue: every path has retired)
+        if (nt > 0 && nready < rtd::kPoolBatch) {
+            // traversal iterations until kPoolBatch paths are ready or no lane traverses; free
+            // lanes are refilled in batches of kPoolRefill
+            int kt = nt;
+            do {
+                const bool done = rtd::trav_step_coop<COUNT, kCoopLeavesPlain>(sc, r, T, S, nodes, cnt, trav,
+                                                                               kCoopRoundMinPlain);
+                if (done) trav = false;
+                finish(done);
+                if (__popcll(__ballot(!trav)) >= rtd::kPoolRefill && qt > qh) refill();
+                kt = __popcll(__ballot(trav));
+            } while (kt > 0 && rt - rh < rtd::kPoolBatch);
+            continue;
+        }
+        // shading pass: lanes 0..ns-1 shade the oldest ready paths; a lane that traverses
+        // another path keeps its frames, the light walk stacks above them
+        const int ns = nready < 64 ? nready : 64;
+        bool push = false, need = false;
+        int js = 0;
+        const int sp0 = trav ? T.sp : 0;
+        if constexpr (kPoolPark) {
+            // park the traversal (its ray is the path record's; the rest in the lane's slot of
+            // WfState::st) so that none of it is live across the shading code (every lane
+            // stores and reloads, so no value of a free lane survives the pass either)
+            {
+                const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                st.st[2 * slot] = make_float4(__uint_as_float(T.a), __uint_as_float(T.b), T.acc,
+                                              __uint_as_float((uint32_t)T.sp | (uint32_t)T.phase << 8 | (uint32_t)jc << 16));
+                st.st[2 * slot + 1] = make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
+            }
+        }
+        if (lane < ns) {
+            js = rr[(unsigned)(rh + lane) % (unsigned)rtd::kPool];
+            rtd::OffsetStack<decltype(S)> os{S, sp0};
+            need = rtd::pool_shade<COUNT>(V, wbase + js, sc, g, st, spp, out, root, os, cnt, push);
+        }
+        if constexpr (kPoolPark) {
+            {
+                const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                const float4 a = st.st[2 * slot], b = st.st[2 * slot + 1];
+                const uint32_t w = __float_as_uint(a.w);
+                T.a = __float_as_uint(a.x);
+                T.b = __float_as_uint(a.y);
+                T.acc = a.z;
+                T.sp = (int)(w & 255u);
+                T.phase = (int)((w >> 8) & 255u);
+                jc = (int)(w >> 16);
+                T.best = rtd::Hit{b.x, b.y, b.z, __float_as_int(b.w)};
+                uint32_t miss;
+                r = rtd::pool_load_ray(V, wbase + jc, miss);
+            }
+        }
+        rh += ns;
+        const int pix = rtd::pool_claim(need, queue, n_items, order, exhausted);
+        if (pix >= 0) rtd::pool_assign(V, wbase + js, sc, g, pix, root);
+        rtd::pool_push(rq, qt, push || pix >= 0, js);
+    }
     rtd::counters_flush<COUNT>(cnt, counters);
 }
 
@@ -774,12 +917,28 @@ void free_device_scene(rt_device_scene *d) {
     if (!d) return;
     DeviceGuard guard(d->device);
     if (guard.ok) {
+        for (hipStream_t q : {d->fr_stream, d->cp_stream})
+            if (q) (void)hipStreamSynchronize(q);
         for (void *p : {d->buf, (void *)d->counters, (void *)d->queue, d->wf_buf, (void *)d->wf_count,
-                        (void *)d->wf_fetch, (void *)d->fast_part, d->order_buf})
+                        (void *)d->wf_fetch, (void *)d->fast_part, d->order_buf, d->fr_buf[0], d->fr_buf[1], d->root_buf})
             if (p) (void)hipFree(p);
         if (d->wf_host_count) (void)hipHostFree(d->wf_host_count);
+        for (hipEvent_t e : {d->fr_copied[0], d->fr_copied[1], d->fr_finished, d->fr_last})
+            if (e) (void)hipEventDestroy(e);
+        for (hipStream_t q : {d->fr_stream, d->cp_stream})
+            if (q) (void)hipStreamDestroy(q);
     }
     delete d;
+}
+
+// rt_render_frame's per-device streams and events (created once per device copy).
+hipError_t ensure_frame_streams(rt_device_scene *d) {
+    hipError_t e = hipSuccess;
+    if (!d->fr_stream) e = hipStreamCreateWithFlags(&d->fr_stream, hipStreamNonBlocking);
+    if (e == hipSuccess && !d->cp_stream) e = hipStreamCreateWithFlags(&d->cp_stream, hipStreamNonBlocking);
+    for (hipEvent_t *ev : {&d->fr_copied[0], &d->fr_copied[1], &d->fr_finished, &d->fr_last})
+        if (e == hipSuccess && !*ev) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    return e;
 }
 
 int ensure_device_scene(rt_scene *s, int device) {
@@ -1056,10 +1215,12 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
         HIP_TRY(hipEventRecord(e0, stream));
     }
     bool ordered = false;
+    uint64_t sched = 0;   // rt_stats.schedule (RT_SCHED_* bit of the kernel that ran)
     if (g.n_pixels > 0) {
         if (p->kernel == RT_KERNEL_WAVEFRONT) {
             int rc = launch_wavefront(d, g, spp, s->ray_depth, d_out, stream, count, timer);
             if (rc) return rc;
+            sched = RT_SCHED_WAVEFRONT;
         } else {   // lane-resident (rt_mega.h), the default
             if (s->ray_depth < 1 || s->ray_depth > 15) return rt_fail(RT_ERR_LIMIT, "ray_depth must be in [1, 15]");
             if (spp >= (1 << 20)) return rt_fail(RT_ERR_LIMIT, "rt_render: spp must be < 2^20");
@@ -1078,20 +1239,32 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const long long full_blocks = resident_blocks(d, rt_mega_kernel<false, false, false, true>);
             const bool spec = !fast && !lsplit && !count && !(p->flags & RT_FLAG_NO_RUNAHEAD) &&
                               g.n_pixels * kClaimStride <= kSpecPixelsPerLane * full_blocks * 256;
+            // path pool (rt_pool.h) for the other parity renders; its light walk stacks above a
+            // traversal's frames, so both BVH depths must fit the stack together
+            const bool pool = !fast && !lsplit && !spec && (p->flags & RT_FLAG_POOL) && kClaimStride == 1 &&
+                              s->bvh_depth + s->light_bvh_depth + 6 < (uint32_t)rtd::kStack;
             auto mk = fast ? (count ? rt_mega_kernel<true, true> : rt_mega_kernel<false, true>)
                            : lsplit ? (count ? rt_mega_kernel<true, false, true> : rt_mega_kernel<false, false, true>)
                                     : count ? rt_mega_kernel<true>
                                             : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
-            const unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
-            int rc = ensure_wf(d, std::max<long long>(g.n_pixels, (long long)blocks * 256), s->ray_depth);   // vertex records
+            sched = fast ? RT_SCHED_FAST : lsplit ? RT_SCHED_LIGHT_SPLIT : spec ? RT_SCHED_RUNAHEAD
+                                                                         : pool ? RT_SCHED_POOL : RT_SCHED_LANE;
+            auto pk = count ? rt_pool_kernel<true> : rt_pool_kernel<false>;
+            // pool: kPool paths per wave, so a block serves 256 x kPoolPerLane pixels at once
+            const unsigned blocks = pool ? persistent_blocks(d, pk, (n_items + rtd::kPoolPerLane - 1) / rtd::kPoolPerLane)
+                                         : persistent_blocks(d, mk, n_items * kClaimStride);
+            const long long slots = (long long)blocks * 256 * (pool ? rtd::kPoolPerLane : 1);   // lane slots / paths
+            int rc = ensure_wf(d, std::max<long long>(g.n_pixels, slots), s->ray_depth);   // vertex records
             if (rc) return rc;
             rtd::WfState w = d->wf;
             w.n = g.n_pixels;
-            w.lanes = (long long)blocks * 256;   // LaneRec slots (<= the workspace capacity)
+            w.lanes = slots;   // LaneRec slots (<= the workspace capacity); the pool's record planes
             w.round_min = d->ds.n_nodes < kCoopRoundNodes ? kCoopRoundMinSpec : 65;
             int *order = nullptr;
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
-                rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
+                // the spread deals one pixel of every cost stratum to each claim of 64 of the
+                // launch's first round (one per wave; kPoolPerLane per wave in the pool)
+                rc = launch_order(d, g, stream, 4LL * blocks * (pool ? rtd::kPoolPerLane : 1), 64, &order);
                 if (rc) return rc;
                 ordered = true;
             }
@@ -1110,8 +1283,12 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
             }
 #endif
-            hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
-                               (const int *)order, (unsigned *)nullptr, cs);
+            if (pool)
+                hipLaunchKernelGGL(pk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
+                                   (const int *)order);
+            else
+                hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
+                                   (const int *)order, (unsigned *)nullptr, cs);
             HIP_TRY(hipGetLastError());
             if (fast) {
                 const long long n3 = g.n_pixels * 3;
@@ -1182,6 +1359,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
         st->render_ms = ms;
         st->order_ms = ms_order;
         st->devices = 1;
+        st->schedule = sched;
         double kms[2];
         uint64_t kn[2];
         HIP_TRY(timer.collect(kms, kn));
@@ -1254,27 +1432,6 @@ __global__ void __launch_bounds__(256) rt_rows_scatter_kernel(const uint8_t *__r
     }
 }
 
-namespace {
-
-// Device buffers released on every return path (on their own device).
-struct DevBuf {
-    int dev = -1;
-    void *p = nullptr;
-    hipError_t alloc(int device, size_t bytes) {
-        dev = device;
-        DeviceGuard g(device);
-        return hipMalloc(&p, bytes ? bytes : 4);
-    }
-    ~DevBuf() {
-        if (p) {
-            DeviceGuard g(dev);
-            (void)hipFree(p);
-        }
-    }
-};
-
-}  // namespace
-
 extern "C" {
 
 int rt_scene_upload(rt_scene *s, int32_t device) {
@@ -1321,12 +1478,19 @@ int rt_render(rt_scene *s, const rt_params *p, float *out, rt_stats *st) {
 // that device's shards one after another (one render per (scene, device) in flight), finishes
 // each to 8 bits on the same device (rt_finish_kernel, scene.cpp:54-64) and copies it, 8-bit
 // frame and (if asked) float sums, device-to-device into a staging buffer on the root device
-// devices[0] (hipMemcpyPeerAsync: over xGMI between MI355X).  The root then places the rows
-// in frame order (rt_rows_scatter_kernel; the reference's canvas, canvas.h:76-89, is row-major)
-// and the frame leaves the devices in one copy per output.
+// devices[0] (hipMemcpyPeerAsync: over xGMI between MI355X) on a copy stream of its own, so
+// the copy of one shard overlaps the render of the device's next one.  The root then places
+// the rows in frame order (rt_rows_scatter_kernel; the reference's canvas, canvas.h:76-89, is
+// row-major) behind an event wait per device, and the frame leaves the devices in one copy per
+// output.  Streams, events and buffers are kept in the scene's device copies between frames.
+// (On the one-GPU pool this runs with every shard on device 0; the peer copies between two
+// MI355X have not run on hardware.)
 int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int32_t *devices, uint8_t *out_rgb,
                     float *out_sum, rt_stats *st) {
     if (!s || !p || (!out_rgb && !out_sum)) return rt_fail(RT_ERR_ARG, "rt_render_frame: NULL argument");
+    // (a devices array needs its length: one entry per shard, so n_shards must be given)
+    if (devices && n_shards <= 0)
+        return rt_fail(RT_ERR_ARG, "rt_render_frame: devices given without n_shards (one device per shard)");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     const int n = n_shards > 0 ? n_shards : ndev;
@@ -1349,26 +1513,37 @@ int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int
     std::vector<int32_t> frame_row_of((size_t)std::max(H, 1));
     for (int r = 0; r < n; ++r) {
         rows[r] = rt_shard_rows_impl(H, r, n, rb, nullptr);
-        if (rows[r] < 0) return RT_ERR_ARG;
+        if (rows[r] < 0) return rt_fail(RT_ERR_ARG, "rt_render_frame: bad row partition (height " + std::to_string(H) +
+                                                        ", row_block " + std::to_string(rb) + ")");
         rt_shard_rows_impl(H, r, n, rb, frame_row_of.data() + base[r]);
         base[r + 1] = base[r] + rows[r];
     }
     const size_t row_u8 = (size_t)W * 3, row_f = row_u8 * sizeof(float);
-    DevBuf stage_u8, stage_f, frame_u8, frame_f, row_map;
-    HIP_TRY(stage_u8.alloc(root, (size_t)H * row_u8));
-    HIP_TRY(frame_u8.alloc(root, (size_t)H * row_u8));
-    if (out_sum) {
-        HIP_TRY(stage_f.alloc(root, (size_t)H * row_f));
-        HIP_TRY(frame_f.alloc(root, (size_t)H * row_f));
-    }
-    HIP_TRY(row_map.alloc(root, (size_t)std::max(H, 1) * sizeof(int32_t)));
-    {
-        DeviceGuard g(root);
-        HIP_TRY(hipMemcpy(row_map.p, frame_row_of.data(), (size_t)H * sizeof(int32_t), hipMemcpyHostToDevice));
-    }
     std::vector<int> uniq;
     for (int d : dev_of)
         if (std::find(uniq.begin(), uniq.end(), d) == uniq.end()) uniq.push_back(d);
+    for (int d : uniq) {   // every device's scene copy, streams and events (kept between frames)
+        rc = ensure_device_scene(s, d);
+        if (rc) return rc;
+        DeviceGuard g(d);
+        HIP_TRY(ensure_frame_streams(s->dev[d]));
+    }
+    // the root's staging (shard r's rows at row offset base[r]), frame buffers and row map:
+    // [stage u8 | frame u8 | stage f32 | frame f32 | frame_row_of], each 256-B aligned
+    rt_device_scene *rd = s->dev[root];
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t b_u8 = al((size_t)H * row_u8), b_f = out_sum ? al((size_t)H * row_f) : 0,
+                 b_map = al((size_t)std::max(H, 1) * sizeof(int32_t));
+    {
+        DeviceGuard g(root);
+        HIP_TRY(grow(&rd->root_buf, &rd->root_bytes, 2 * b_u8 + 2 * b_f + b_map));
+        HIP_TRY(hipStreamSynchronize(rd->fr_stream));   // (the previous frame's map upload is done)
+        HIP_TRY(hipMemcpyAsync((uint8_t *)rd->root_buf + 2 * b_u8 + 2 * b_f, frame_row_of.data(),
+                               (size_t)H * sizeof(int32_t), hipMemcpyHostToDevice, rd->fr_stream));
+    }
+    uint8_t *stage_u8 = (uint8_t *)rd->root_buf, *frame_u8 = stage_u8 + b_u8;
+    uint8_t *stage_f = frame_u8 + b_u8, *frame_f = stage_f + b_f;
+    const int *row_map = (const int *)(frame_f + b_f);
     for (int d : uniq) {   // direct xGMI copies between the root and its peers where the runtime allows
         if (d == root) continue;
         int can = 0;
@@ -1386,75 +1561,92 @@ int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int
     std::vector<int> rcs(uniq.size(), RT_OK);
     std::vector<std::string> errs(uniq.size());
     std::vector<rt_stats> sts(n);
-    std::vector<double> copy_ms(uniq.size(), 0.0);
+    // One host thread per device.  Its shards alternate between two buffers: shard r is
+    // rendered (launch waits for it: stats) and finished to 8 bits on the render stream; the
+    // copy stream waits for that finish and copies the shard to the root's staging buffer,
+    // while the render stream goes on with the next shard in the other buffer (it waits for
+    // that buffer's previous copy first).  The device's last copy is marked by fr_last, which
+    // the root's assembly waits for on the device, not on the host.
     auto work = [&](size_t ui) {
         const int dev = uniq[ui];
+        rt_device_scene *dd = s->dev[dev];
         auto fail = [&](int code, const std::string &m) {
             rcs[ui] = rt_fail(code, m);
             errs[ui] = rt_last_error();
         };
-        int r0 = ensure_device_scene(s, dev);
-        if (r0) { rcs[ui] = r0; errs[ui] = rt_last_error(); return; }
         DeviceGuard g(dev);
         if (!g.ok) return fail(RT_ERR_DEVICE, "hipSetDevice failed");
-        hipStream_t stream = nullptr;
-        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
-            return fail(RT_ERR_DEVICE, "hipStreamCreate failed");
         int64_t max_rows = 0;
         for (int r = 0; r < n; ++r)
             if (dev_of[r] == dev) max_rows = std::max(max_rows, rows[r]);
-        DevBuf sum, rgb;
-        hipError_t e = sum.alloc(dev, (size_t)max_rows * row_f);
-        if (e == hipSuccess) e = rgb.alloc(dev, (size_t)max_rows * row_u8);
+        const size_t b_sum = al((size_t)max_rows * row_f);
+        hipError_t e = hipSuccess;
+        for (int b = 0; b < 2 && e == hipSuccess; ++b) e = grow(&dd->fr_buf[b], &dd->fr_bytes[b], b_sum + (size_t)max_rows * row_u8);
+        int nb = 0;   // shards done on this device (buffer = nb % 2)
         for (int r = 0; r < n && e == hipSuccess && rcs[ui] == RT_OK; ++r) {
             if (dev_of[r] != dev || rows[r] == 0) continue;
+            const int b = nb % 2;
+            float *sum = (float *)dd->fr_buf[b];
+            uint8_t *rgb = (uint8_t *)dd->fr_buf[b] + b_sum;
+            if (nb >= 2) e = hipStreamWaitEvent(dd->fr_stream, dd->fr_copied[b], 0);   // buffer b's last copy done
+            if (e != hipSuccess) break;
             rt_params q = *p;
             q.rank = r;
             q.world = n;
             q.row_block = rb;
             q.device = dev;
             q.spp = spp;
-            int lr = launch(s, &q, (float *)sum.p, stream, &sts[r]);   // waits (stats)
+            int lr = launch(s, &q, sum, dd->fr_stream, &sts[r]);   // waits (stats)
             if (lr) { rcs[ui] = lr; errs[ui] = rt_last_error(); break; }
-            lr = rt_tonemap_u8_device((const float *)sum.p, W, (int32_t)rows[r], spp, (uint8_t *)rgb.p, stream);
+            lr = rt_tonemap_u8_device(sum, W, (int32_t)rows[r], spp, rgb, dd->fr_stream);
             if (lr) { rcs[ui] = lr; errs[ui] = rt_last_error(); break; }
-            const auto t0 = std::chrono::steady_clock::now();
-            e = hipMemcpyPeerAsync((uint8_t *)stage_u8.p + base[r] * row_u8, root, rgb.p, dev, rows[r] * row_u8, stream);
+            e = hipEventRecord(dd->fr_finished, dd->fr_stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(dd->cp_stream, dd->fr_finished, 0);
+            if (e == hipSuccess)
+                e = hipMemcpyPeerAsync(stage_u8 + base[r] * row_u8, root, rgb, dev, rows[r] * row_u8, dd->cp_stream);
             if (e == hipSuccess && out_sum)
-                e = hipMemcpyPeerAsync((uint8_t *)stage_f.p + base[r] * row_f, root, sum.p, dev, rows[r] * row_f, stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(stream);
-            copy_ms[ui] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                e = hipMemcpyPeerAsync(stage_f + base[r] * row_f, root, sum, dev, rows[r] * row_f, dd->cp_stream);
+            if (e == hipSuccess) e = hipEventRecord(dd->fr_copied[b], dd->cp_stream);
+            ++nb;
         }
+        if (e == hipSuccess) e = hipEventRecord(dd->fr_last, dd->cp_stream);
         if (e != hipSuccess && rcs[ui] == RT_OK) fail(RT_ERR_DEVICE, std::string("rt_render_frame: ") + hipGetErrorString(e));
-        (void)hipStreamDestroy(stream);
     };
     std::vector<std::thread> threads;
     for (size_t ui = 1; ui < uniq.size(); ++ui) threads.emplace_back(work, ui);
     work(0);
     for (std::thread &t : threads) t.join();
-    for (size_t ui = 0; ui < uniq.size(); ++ui)
-        if (rcs[ui] != RT_OK) return rt_fail(rcs[ui], "device " + std::to_string(uniq[ui]) + ": " + errs[ui]);
-    // assemble on the root, one copy to the host per output
+    // every shard's render has ended here (launch waited for each); from now on the host waits
+    // only for the copies still in flight, the assembly and the copy to the host: gather_ms
     const auto t0 = std::chrono::steady_clock::now();
-    {
+    for (size_t ui = 0; ui < uniq.size(); ++ui)
+        if (rcs[ui] != RT_OK) {
+            for (int d : uniq) {   // (leave no copy in flight into the root's buffers)
+                DeviceGuard g(d);
+                (void)hipStreamSynchronize(s->dev[d]->cp_stream);
+            }
+            return rt_fail(rcs[ui], "device " + std::to_string(uniq[ui]) + ": " + errs[ui]);
+        }
+    {   // assemble on the root behind every device's last copy, one copy to the host per output
         DeviceGuard g(root);
         if (!g.ok) return rt_fail(RT_ERR_DEVICE, "hipSetDevice failed");
+        hipStream_t q = rd->fr_stream;
+        for (int d : uniq) HIP_TRY(hipStreamWaitEvent(q, s->dev[d]->fr_last, 0));
         if (H > 0) {
-            hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(4, (unsigned)H), dim3(256), 0, nullptr,
-                               (const uint8_t *)stage_u8.p, (uint8_t *)frame_u8.p, (const int *)row_map.p, (long long)H,
-                               (long long)row_u8);
+            hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(4, (unsigned)H), dim3(256), 0, q, (const uint8_t *)stage_u8,
+                               frame_u8, row_map, (long long)H, (long long)row_u8);
             HIP_TRY(hipGetLastError());
             if (out_sum) {
-                hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(8, (unsigned)H), dim3(256), 0, nullptr,
-                                   (const uint8_t *)stage_f.p, (uint8_t *)frame_f.p, (const int *)row_map.p,
-                                   (long long)H, (long long)row_f);
+                hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(8, (unsigned)H), dim3(256), 0, q,
+                                   (const uint8_t *)stage_f, frame_f, row_map, (long long)H, (long long)row_f);
                 HIP_TRY(hipGetLastError());
             }
         }
-        if (out_rgb) HIP_TRY(hipMemcpy(out_rgb, frame_u8.p, (size_t)H * row_u8, hipMemcpyDeviceToHost));
-        if (out_sum) HIP_TRY(hipMemcpy(out_sum, frame_f.p, (size_t)H * row_f, hipMemcpyDeviceToHost));
+        if (out_rgb) HIP_TRY(hipMemcpyAsync(out_rgb, frame_u8, (size_t)H * row_u8, hipMemcpyDeviceToHost, q));
+        if (out_sum) HIP_TRY(hipMemcpyAsync(out_sum, frame_f, (size_t)H * row_f, hipMemcpyDeviceToHost, q));
+        HIP_TRY(hipStreamSynchronize(q));
     }
-    const double assemble_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double gather_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (st) {
         std::memset(st, 0, sizeof *st);
         std::vector<double> dev_ms(uniq.size(), 0.0), dev_order(uniq.size(), 0.0);   // a device's shards run in turn
@@ -1464,13 +1656,14 @@ int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int
             st->aabb_tests += x.aabb_tests; st->tri_tests += x.tri_tests; st->light_queries += x.light_queries;
             st->light_aabb_tests += x.light_aabb_tests; st->light_tri_tests += x.light_tri_tests;
             st->shading_hits += x.shading_hits; st->extend_rays += x.extend_rays;
+            st->schedule |= x.schedule;
             const size_t ui = (size_t)(std::find(uniq.begin(), uniq.end(), dev_of[r]) - uniq.begin());
             dev_ms[ui] += x.render_ms;
             dev_order[ui] += x.order_ms;
         }
         st->render_ms = *std::max_element(dev_ms.begin(), dev_ms.end());
         st->order_ms = *std::max_element(dev_order.begin(), dev_order.end());
-        st->gather_ms = *std::max_element(copy_ms.begin(), copy_ms.end()) + assemble_ms;
+        st->gather_ms = gather_ms;
         st->devices = (uint64_t)uniq.size();
     }
     return RT_OK;
@@ -1556,29 +1749,178 @@ __global__ void __launch_bounds__(256) decode_check_kernel(unsigned long long *b
     }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2147483647ull;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t x = (uint32_t)i, f = (uint32_t)(i & 1u);
-        uint32_t ux, uf;
-        rtd::rng_word_unpack(rtd::rng_word_pack(x, f), ux, uf);
-        local += (ux != x) | (uf != f);
+        const uint32_t x = (uint32_t)i;
+#pragma unroll
+        for (uint32_t f = 0; f < 2; ++f) {
+            uint32_t ux, uf;
+            rtd::rng_word_unpack(rtd::rng_word_pack(x, f), ux, uf);
+            local += (ux != x) | (uf != f);
+        }
     }
     for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
     if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
 }
 
+}  // extern "C"
+
+// rt_device_selfcheck 2: the cooperative leaf step (rt_wavefront.h trav_step_coop: four
+// helper lanes per leaf lane, DPP quad min with the triangle index as tie-break, NaN t as no
+// hit, several leaf rounds) against the per-lane sequential loop of trav_step (the reference's
+// in-order strict < of bvh.cpp:226-232 over primitive.cpp:17-57).  Leaves of 1-7 triangles
+// over groups rich in exact duplicates (equal t, u, v), coplanar triangles (equal t), NaN and
+// infinite vertices; every lane of a 256-thread block is a leaf lane, so each step serves 8 of
+// a wave's 64 and the rest wait.  Both round policies (one round per step; rounds until every
+// leaf lane is served).  One mismatching field of a case counts once.
+template <int kLeaves>
+__global__ void __launch_bounds__(256) coop_check_kernel(const float4 *tri, int n_tris, const float4 *nodes,
+                                                          const float4 *rays, const uint2 *leaves, int n_cases,
+                                                          int round_min, unsigned long long *bad) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const bool valid = i < n_cases;
+    DevScene sc{};
+    sc.tri = tri;
+    sc.n_tris = n_tris;
+    sc.node = nodes;
+    sc.n_nodes = 2;
+    const float4 ro = rays[2 * (valid ? i : 0)], rdv = rays[2 * (valid ? i : 0) + 1];
+    const rtd::Ray r = rtd::make_ray(rtv::V3{ro.x, ro.y, ro.z}, rtv::V3{rdv.x, rdv.y, rdv.z});
+    const uint2 lf = leaves[valid ? i : 0];
+    rtd::TravState T;
+    T.best.t = 1e9f;
+    T.best.u = T.best.v = 0.f;
+    T.best.prim = -1;
+    T.acc = 1e9f;
+    T.sp = 0;
+    T.a = T.b = 0;
+    T.k = lf.x;
+    T.kend = lf.y;
+    T.phase = rtd::TP_LEAF;
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    uint2 spill[rtd::kStack - 4];
+    rtd::LdsStackT<4> S{spill};
+    const rtd::GlobalNodes gn{nodes};
+    bool active = valid;
+    for (int it = 0; it < 64 && __any(active); ++it)   // (bounded: 7 triangles, 64 lanes, 8 per round)
+        if (rtd::trav_step_coop<false, kLeaves>(sc, r, T, S, gn, cnt, active, round_min)) active = false;
+    // sequential reference: trav_step's per-lane loop, one triangle at a time
+    float acc = 1e9f;
+    rtd::Hit best{1e9f, 0.f, 0.f, -1};
+    for (uint32_t k = lf.x; valid && k < lf.y; ++k) {
+        const float4 q0 = tri[3 * k], q1 = tri[3 * k + 1], q2 = tri[3 * k + 2];
+        rtd::TriHit h;
+        if (rtd::tri_hit_bl(rtv::V3{q0.x, q0.y, q0.z}, rtv::V3{q0.w, q1.x, q1.y}, rtv::V3{q1.z, q1.w, q2.x}, r, h)) {
+            acc = h.t < acc ? h.t : acc;
+            if (h.t < best.t) best = rtd::Hit{h.t, h.u, h.v, (int)k};
+        }
+    }
+    unsigned long long local = 0;
+    if (valid)
+        local = (active | (T.best.prim != best.prim) | (__float_as_uint(T.best.t) != __float_as_uint(best.t)) |
+                 (__float_as_uint(T.best.u) != __float_as_uint(best.u)) |
+                 (__float_as_uint(T.best.v) != __float_as_uint(best.v)) | (__float_as_uint(T.acc) != __float_as_uint(acc)))
+                    ? 1ull : 0ull;
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
+}
+
+namespace {
+// Host-made cases of selfcheck 2 (deterministic): 8-triangle groups of a base triangle, its
+// exact copy, a coplanar one behind an equal-t prefix, its copy, a NaN-vertex one, a random
+// one, the base again and an infinite-vertex one; rays from random origins at the base's
+// centroid (jittered); leaves of 1-7 consecutive triangles.
+void coop_cases(std::vector<float> &tri, std::vector<float> &rays, std::vector<uint32_t> &leaves, int n_cases) {
+    uint64_t x = 0x9e3779b97f4a7c15ull;
+    auto rnd = [&]() {   // [0, 1)
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        return (float)((x >> 40) & 0xffffff) / 16777216.f;
+    };
+    const int groups = 512;
+    tri.assign((size_t)groups * 8 * 12, 0.f);
+    std::vector<float> cen((size_t)groups * 3);
+    for (int gi = 0; gi < groups; ++gi) {
+        float v0[3], U[3], V[3];
+        for (int c = 0; c < 3; ++c) {
+            v0[c] = rnd() * 4.f - 2.f;
+            U[c] = rnd() * 2.f - 1.f;
+            V[c] = rnd() * 2.f - 1.f;
+            cen[3 * gi + c] = v0[c] + (U[c] + V[c]) / 3.f;
+        }
+        for (int t = 0; t < 8; ++t) {
+            float *o = &tri[((size_t)gi * 8 + t) * 12];
+            float a[3], u[3], w[3];
+            for (int c = 0; c < 3; ++c) {
+                a[c] = v0[c]; u[c] = U[c]; w[c] = V[c];
+                if (t == 2 || t == 3) { a[c] = v0[c] + 0.25f * U[c]; }   // same plane, shifted: equal t, other u
+                if (t == 5) { a[c] = rnd() * 4.f - 2.f; u[c] = rnd() * 2.f - 1.f; w[c] = rnd() * 2.f - 1.f; }
+            }
+            if (t == 4) a[1] = __builtin_nanf("");
+            if (t == 7) u[0] = __builtin_inff();
+            for (int c = 0; c < 3; ++c) { o[c] = a[c]; o[3 + c] = u[c]; o[6 + c] = w[c]; }
+        }
+    }
+    rays.assign((size_t)n_cases * 8, 0.f);
+    leaves.assign((size_t)n_cases * 2, 0u);
+    for (int i = 0; i < n_cases; ++i) {
+        const int gi = (int)(rnd() * groups) % groups;
+        float o[3], d[3];
+        for (int c = 0; c < 3; ++c) {
+            o[c] = rnd() * 20.f - 10.f;
+            d[c] = cen[3 * gi + c] + (rnd() - 0.5f) * 0.2f - o[c];
+        }
+        for (int c = 0; c < 3; ++c) { rays[8 * (size_t)i + c] = o[c]; rays[8 * (size_t)i + 4 + c] = d[c]; }
+        const uint32_t len = 1u + (uint32_t)(rnd() * 7.f) % 7u, first = (uint32_t)gi * 8u + (uint32_t)(rnd() * 8.f) % 8u;
+        const uint32_t k0 = std::min<uint32_t>(first, (uint32_t)groups * 8u - len);
+        leaves[2 * (size_t)i] = k0;
+        leaves[2 * (size_t)i + 1] = k0 + len;
+    }
+}
+}  // namespace
+
+extern "C" {
+
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
     if (!mismatches) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: null output");
-    if (which != 0 && which != 1) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
+    if (which < 0 || which > 2) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
     unsigned long long *d = nullptr;
     HIP_TRY(hipMalloc((void **)&d, sizeof *d));
     hipError_t e = hipMemset(d, 0, sizeof *d);
+    void *cbuf = nullptr;
     if (e == hipSuccess) {
-        if (which == 0) hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
-        else hipLaunchKernelGGL(decode_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
-        e = hipGetLastError();
+        if (which == 0) {
+            hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
+        } else if (which == 1) {
+            hipLaunchKernelGGL(decode_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
+        } else {
+            const int n_cases = 1 << 16;
+            std::vector<float> tri, rays;
+            std::vector<uint32_t> leaves;
+            coop_cases(tri, rays, leaves, n_cases);
+            const size_t bt = tri.size() * 4 + 64, br = rays.size() * 4, bl = leaves.size() * 4, bn = 256;
+            e = hipMalloc(&cbuf, bt + br + bl + bn);
+            uint8_t *b = (uint8_t *)cbuf;
+            if (e == hipSuccess) e = hipMemset(cbuf, 0, bt + br + bl + bn);
+            if (e == hipSuccess) e = hipMemcpy(b, tri.data(), tri.size() * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(b + bt, rays.data(), br, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(b + bt + br, leaves.data(), bl, hipMemcpyHostToDevice);
+            const int n_tris = (int)(tri.size() / 12);
+            const unsigned blocks = (unsigned)(n_cases / 256);
+            if (e == hipSuccess) {
+                for (int rm : {65, 1}) {   // one round per step; every leaf lane served in the step
+                    hipLaunchKernelGGL(coop_check_kernel<8>, dim3(blocks), dim3(256), 0, nullptr, (const float4 *)b,
+                                       n_tris, (const float4 *)(b + bt + br + bl), (const float4 *)(b + bt),
+                                       (const uint2 *)(b + bt + br), n_cases, rm, d);
+                    hipLaunchKernelGGL(coop_check_kernel<16>, dim3(blocks), dim3(256), 0, nullptr, (const float4 *)b,
+                                       n_tris, (const float4 *)(b + bt + br + bl), (const float4 *)(b + bt),
+                                       (const uint2 *)(b + bt + br), n_cases, rm, d);
+                }
+            }
+        }
+        if (e == hipSuccess) e = hipGetLastError();
     }
     unsigned long long h = 0;
     if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
     (void)hipFree(d);
+    if (cbuf) (void)hipFree(cbuf);
     if (e != hipSuccess) return rt_fail(RT_ERR_DEVICE, std::string("rt_device_selfcheck: ") + hipGetErrorString(e));
     *mismatches = h;
     return RT_OK;

@@ -39,9 +39,9 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 4
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 5
     assert ctypes.sizeof(rt.RtParams) == 36
-    assert ctypes.sizeof(rt.RtStats) == 9 * 8 + 3 * 8 + 3 * 8 + 3 * 8
+    assert ctypes.sizeof(rt.RtStats) == 9 * 8 + 3 * 8 + 3 * 8 + 3 * 8 + 8   # ABI 5: + schedule
 
 
 @pytest.mark.parametrize("height,world,rb", [(1080, 1, 8), (1080, 2, 8), (1080, 3, 8), (1080, 8, 8), (17, 3, 4),
@@ -94,6 +94,9 @@ def test_errors_are_reported(rt, tmp_path):
     out = np.zeros(8 * 8 * 3, np.float32)
     assert lib.rt_render_multi(s.handle, ctypes.byref(p), 1, None, None) == -1   # RT_ERR_ARG
     assert lib.rt_render_frame(s.handle, ctypes.byref(p), 1, None, None, None, None) == -1   # no output
+    dev = (ctypes.c_int32 * 2)(0, 0)   # a devices array needs n_shards (its length)
+    assert lib.rt_render_frame(s.handle, ctypes.byref(p), 0, dev, None, out.ctypes.data_as(rt._c_f), None) == -1
+    assert b"n_shards" in lib.rt_last_error()
     if rt.device_count() == 0:   # no GPU: every render entry fails loudly (no CPU fallback)
         assert lib.rt_render(s.handle, ctypes.byref(p), out.ctypes.data_as(rt._c_f), None) == -4   # RT_ERR_DEVICE
         assert lib.rt_render_multi(s.handle, ctypes.byref(p), 0, out.ctypes.data_as(rt._c_f), None) == -4

@@ -7,9 +7,11 @@ sources, oracle/ref_harness `pixels`, per-pixel RNG convention of SURVEY.md §8c
   C4        sponza proxy 1920x1080x1024, each of the 8 row-block shards of the 8-GPU split
   C5        dragon-100k + sponza proxy 3840x2160x4096, rank 0's shard of the 8-GPU split, and
             64 pixels of each of ranks 1-7 at full spp
-  whole frames: C3 and the headline, every row of the float frame (per-row FNV-1a hashes of
-            the reference's own full render, tools/make_goldens.py --frames), 8 full rows,
-            the frame counters, and the sha1 of the reference's finished 8-bit frame
+  whole frames: C3 and the headline (and C4 once its golden exists), every row of the float
+            frame (per-row FNV-1a hashes of the reference's own full render,
+            tools/make_goldens.py --frames), 8 full rows, the frame counters, and the sha1 of
+            the reference's finished 8-bit frame; rendered on one GPU (the plain kernel) and as
+            the 4- and 8-way splits (the runahead kernel), reassembled
 
 These are the frames whose per-pixel sample chains (256 to 4096 sequential samples, RNG
 state and pixel sum held in LDS between uses: rt_mega.h) the small parity cases cannot reach.
@@ -132,6 +134,35 @@ def test_c5_ranks_1_to_7_match_reference(gpu):
         out, _ = scene.render_sums(S, rank=rank, world=world)
         checked += _check(out, gpu.shard_rows(H, rank, world), W, g, world, rank)
     assert checked == len(g["index"]) == 64 * len(c["ranks"])
+
+
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("config", sorted(FRAMES))
+def test_split_frame_runahead_matches_reference(gpu, config, world):
+    """The whole BASELINE frame as the shards of the 4- and 8-way split, each rendered by the
+    runahead kernel (rt_mega.h spec_manage: one and two pixels per lane), reassembled and
+    compared row by row with the reference's own render of the frame (every row's FNV-1a
+    hash, 8 full rows; scene.cpp:31-64).  The 8-way split also goes through rt_render_frame
+    (each shard finished to 8 bits on the device and gathered there), whose 8-bit frame must
+    be the reference's PPM body (canvas.h:76-89)."""
+    import hashlib
+    f = FRAMES[config]
+    W, H, S = f["width"], f["height"], f["spp"]
+    scene = _scene(gpu, f["scene"], W, H, S)
+    frame = np.full((H, W, 3), np.nan, np.float32)
+    for rank in range(world):
+        rows = gpu.shard_rows(H, rank, world)
+        part, st = scene.render_sums(S, rank=rank, world=world)
+        assert st["schedule"] == gpu.SCHED_RUNAHEAD, f"rank {rank}: schedule {st['schedule']}"
+        frame[rows] = part
+    g = rtref.golden(f["file"])
+    bad = np.nonzero(rtref.row_hash(frame) != g["row_fnv1a"])[0]
+    assert len(bad) == 0, f"{len(bad)} of {H} rows differ, first {bad[:8]}"
+    assert np.array_equal(rtref.bits(frame[g["rows"]]), rtref.bits(g["row_sums"]))
+    if world == 8:
+        rgb, _, st = scene.render_frame(S, n_shards=8, devices=[0] * 8, sums=False)
+        assert st["schedule"] == gpu.SCHED_RUNAHEAD
+        assert hashlib.sha1(rgb.tobytes()).hexdigest() == f["frame_u8_sha1"]
 
 
 @pytest.mark.parametrize("config", sorted(FRAMES))

@@ -52,6 +52,49 @@ def test_sums_match_reference(gpu, name, w, h, s, kernel, order):
             st["light_tri_tests"]] == [int(x) for x in c]
 
 
+@pytest.mark.parametrize("count,order", [(True, "heavy"), (True, "natural"), (False, "heavy"), (False, "natural")])
+@pytest.mark.parametrize("name,w,h,s", CASES)
+def test_pool_matches_reference(gpu, name, w, h, s, count, order):
+    """The path-pool schedule (rt_pool.h: a wave's 128 paths in HBM, lanes as traversal slots
+    fed from the wave's queue, ready paths shaded 64 at a time; RT_FLAG_POOL) against the
+    reference's sums, and its traversal counters where counting, in both pixel orders.  These
+    frames have fewer pixels than lanes, so a wave's pool is partly empty from the start and
+    the frame is all tail (runahead off, so the pool takes them)."""
+    scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
+    out, st = _sums(scene, s, count=count, pool=True, runahead=False, natural_order=order == "natural",
+                    heavy_order=order == "heavy")
+    assert st["schedule"] == gpu.SCHED_POOL
+    g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
+    ref = g["sums"].reshape(-1, 3)
+    bad = (rtref.bits(out) != rtref.bits(ref)).any(1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ, max |d| {np.abs(out - ref).max()}"
+    if count:
+        c = g["counters"]
+        assert [st["rays"], st["aabb_tests"], st["tri_tests"], st["light_queries"], st["light_aabb_tests"],
+                st["light_tri_tests"]] == [int(x) for x in c]
+
+
+def test_pool_many_pixels_per_path_vs_oracle(gpu, oracle):
+    """The pool where every path runs several pixels (a 1920x1080 frame: 2.07 M pixels for at
+    most 655 k paths), 16-sample chains, translucent materials and both orders: the frame
+    equals the lane-resident kernel's, and sampled pixels equal the CPU oracle."""
+    name, W, H, S = "sponza_mini", 1920, 1080, 16
+    a = rtref.ref_arrays(gpu, name, W, H, S)
+    a["mesh_f"] = a["mesh_f"].copy()
+    a["mesh_f"][::3, 8] = np.float32(0.5)
+    scene = gpu.Scene.from_view(a)
+    lane, st0 = scene.render_sums(S, runahead=False, heavy_order=True)
+    pool, st1 = scene.render_sums(S, pool=True, runahead=False, heavy_order=True)
+    pool_n, _ = scene.render_sums(S, pool=True, runahead=False, natural_order=True)
+    assert st0["schedule"] == gpu.SCHED_LANE and st1["schedule"] == gpu.SCHED_POOL
+    assert np.array_equal(rtref.bits(lane), rtref.bits(pool))
+    assert np.array_equal(rtref.bits(lane), rtref.bits(pool_n))
+    rng = np.random.default_rng(5)
+    for p in rng.choice(W * H, 10, replace=False):
+        ref, _, _ = oracle.render(a, S, int(p), int(p) + 1, threads=1)
+        assert np.array_equal(rtref.bits(pool.reshape(-1, 3)[p]), rtref.bits(ref[0])), f"pixel {p}"
+
+
 @pytest.mark.parametrize("name,w,h,s", CASES)
 def test_loader_path_matches_reference(gpu, name, w, h, s):
     """Own glTF loader + BVH builder (rt_scene_load_gltf) -> GPU: same bits as the reference
@@ -320,6 +363,33 @@ def test_texel_decode_and_rng_word_are_exact(gpu):
     byte, and the packed LDS RNG word round-trips for every minstd state and both cache flags,
     on the device (rt_device_selfcheck 1)."""
     assert gpu.device_selfcheck(1) == 0
+
+
+def test_coop_leaf_step_ties_and_nan(gpu):
+    """The cooperative leaf step (rt_wavefront.h trav_step_coop: four helper lanes per leaf
+    lane, DPP quad min with the triangle index as tie-break, NaN t as no hit) against the
+    per-lane in-order strict-< loop (bvh.cpp:226-232 over primitive.cpp:17-57) on 2^16
+    synthetic leaves of 1-7 triangles full of exact duplicates (equal t, u, v), coplanar
+    triangles (equal t), NaN and infinite vertices, with one round per step and with every
+    leaf lane served per step, 8 and 16 leaf records (rt_device_selfcheck 2)."""
+    assert gpu.device_selfcheck(2) == 0
+
+
+def test_schedule_reported(gpu):
+    """rt_stats.schedule names the kernel that rendered: the plain lane-resident kernel for a
+    frame of more pixels than lanes (or a counting render), the runahead kernel for its 8-way
+    shards, fast mode, the light-split kernel and the wavefront launches."""
+    scene = gpu.Scene.load(rtref.scene_path("sponza_mini"), 64, 36, 4)
+    big = gpu.Scene.load(rtref.scene_path("sponza_mini"), 1280, 720, 1)
+    assert big.render_sums(1)[1]["schedule"] == gpu.SCHED_LANE
+    assert scene.render_sums(4, count=True)[1]["schedule"] == gpu.SCHED_LANE
+    assert scene.render_sums(4, rank=1, world=8)[1]["schedule"] == gpu.SCHED_RUNAHEAD
+    assert scene.render_sums(4, runahead=False)[1]["schedule"] == gpu.SCHED_LANE
+    assert scene.render_sums(4, fast=True)[1]["schedule"] == gpu.SCHED_FAST
+    assert scene.render_sums(4, light_split=True)[1]["schedule"] == gpu.SCHED_LIGHT_SPLIT
+    assert scene.render_sums(4, kernel=4)[1]["schedule"] == gpu.SCHED_WAVEFRONT
+    _, _, st = scene.render_frame(4, devices=[0] * 8, sums=False)
+    assert st["schedule"] == gpu.SCHED_RUNAHEAD
 
 
 @pytest.mark.parametrize("name,w,h,s", CASES)

@@ -152,7 +152,8 @@ def config_goldens(meta):
         print(name, meta["configs"][name]["pixels"], flush=True)
 
 
-FRAMES = [("c3", "sponza", 1024, 1024, 256), ("headline", "sponza", 1920, 1080, 256)]
+FRAMES = [("c3", "sponza", 1024, 1024, 256), ("headline", "sponza", 1920, 1080, 256),
+          ("c4", "sponza", 1920, 1080, 1024)]   # C4 whole frame: about 1.8 h on 8 threads here
 C5_RANKS_PIXELS = 64     # pixels per rank for the every-rank C5 golden
 
 

@@ -1,7 +1,9 @@
 #!/bin/bash
 # SQ counter passes over one rank's shard (tools/shard_time.py) per world size, to compare
 # where wave time goes at full and at low occupancy.  One rocprofv3 --pmc pass per run.
-#   bash tools/pmc_shard.sh TAG "8 128" [pass ...]        (passes: sq1 sq2; default both)
+#   bash tools/pmc_shard.sh TAG "8 128" [pass ...]        (passes: sq1 sq2 sq3 fetch write tcc; default sq1 sq2)
+# gpurun_out/pmc_TAG/<pass>_w<N>.csv; committed as profiles/<TAG>_shard_<pass>_w<N>.csv (bench.py
+# reads those for an --gpus N line).
 set -o pipefail
 cd "$(dirname "$0")/.."
 TAG=$1; WORLDS=$2; shift 2
@@ -12,7 +14,10 @@ export TMPDIR=/tmp
 for w in $WORLDS; do
   for p in $PASSES; do
     case $p in
-      sq1) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CYCLES" ;;
+      sq1) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" ;;
+      fetch) C="FETCH_SIZE" ;;
+      write) C="WRITE_SIZE" ;;
+      tcc) C="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" ;;
       sq2) C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INST_LEVEL_VMEM SQ_INSTS_LDS" ;;
       sq3) C="SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_EXP SQ_LDS_BANK_CONFLICT" ;;
     esac
