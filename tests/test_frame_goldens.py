@@ -1,5 +1,5 @@
 """The whole-frame goldens of the BASELINE frames (tools/make_goldens.py --frames: the
-reference's own render of C3 and the headline, scene.cpp:31-64) are self-consistent, and the
+reference's own render of C3, the headline and C4, scene.cpp:31-64) are self-consistent, and the
 host frame finish (rt_tonemap_u8, scene.cpp:54-64) turns their float rows into the
 reference's 8-bit rows.  CPU only; the GPU comparison is tests/test_gpu_configs.py
 test_whole_frame_matches_reference."""
@@ -14,7 +14,7 @@ import rtref
 FRAMES = json.load(open(os.path.join(rtref.GOLD, "golden_meta.json"))).get("frames", {})
 
 
-@pytest.mark.parametrize("config", ["c3", "headline"])
+@pytest.mark.parametrize("config", ["c3", "headline", "c4"])
 def test_frame_golden_is_consistent(rt, config):
     f = FRAMES[config]
     W, H, S = f["width"], f["height"], f["spp"]
@@ -39,4 +39,5 @@ def test_bench_knows_the_reference_frame():
         sys.argv = argv
     f = FRAMES["headline"]
     assert b.reference_frame_sha1("sponza", 1920, 1080, 256) == f["frame_u8_sha1"]
-    assert b.reference_frame_sha1("sponza", 1920, 1080, 1024) is None
+    assert b.reference_frame_sha1("sponza", 1920, 1080, 1024) == FRAMES["c4"]["frame_u8_sha1"]
+    assert b.reference_frame_sha1("sponza", 1920, 1080, 64) is None
