@@ -80,6 +80,12 @@ constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #define RT_PLAIN_TRAV_SHARED 1
 #endif
 constexpr bool kPlainTravShared = RT_PLAIN_TRAV_SHARED != 0;
+// The lane-resident kernel parks its lanes' traversal state in memory around a shading pass
+// (rt_mega_kernel); 0: kept in registers (the compiler spills it), for A/B builds.
+#ifndef RT_PARK_TRAV
+#define RT_PARK_TRAV 1
+#endif
+constexpr bool kParkTrav = RT_PARK_TRAV != 0;
 // ... whose leaf work is spread over the wave (rt_wavefront.h trav_step_coop).  0: per-lane
 // leaf steps of RT_LEAF_N triangles, for A/B builds.
 #ifndef RT_COOP_LEAF
@@ -432,6 +438,34 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 pf[6] += (unsigned long long)kt;
 #endif
             } while (true);
+        } else if (kParkTrav && !kSpec && !LSPLIT && shade_now) {
+            // Shading pass with the traversal state parked: every lane stores its ray and
+            // traversal state to its lane slot of WfState::mid before the pass, and a lane that
+            // did not start a new ray in the pass (it was traversing, or went idle) reloads it
+            // after, so none of it is live across the shading code (which the compiler would
+            // otherwise spill and reload around the pass and at the loop's back-edge).
+            const long long slot = rtd::mega_slot(), ln = st.lanes;
+            float4 *pk = st.mid;
+            pk[slot] = make_float4(L.r.o.x, L.r.o.y, L.r.o.z, __uint_as_float(L.T.a));
+            pk[ln + slot] = make_float4(L.r.d.x, L.r.d.y, L.r.d.z, __uint_as_float(L.T.b));
+            pk[2 * ln + slot] = make_float4(L.T.best.t, L.T.best.u, L.T.best.v, __int_as_float(L.T.best.prim));
+            pk[3 * ln + slot] = make_float4(L.T.acc, __uint_as_float((uint32_t)L.T.sp | (uint32_t)L.T.phase << 8), 0.f, 0.f);
+            const bool was_ready = L.state == rtd::M_READY;
+            rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, true, sc, g, st, spp, out, cost,
+                                                                               root, S, nodes, cnt, false);
+            const bool fresh = was_ready && (L.state == rtd::M_TRAV || L.state == rtd::M_READY);   // a new ray
+            if (!fresh) {
+                const float4 a = pk[slot], b = pk[ln + slot], c = pk[2 * ln + slot], d = pk[3 * ln + slot];
+                L.r.o = rtv::V3{a.x, a.y, a.z};
+                L.r.d = rtv::V3{b.x, b.y, b.z};
+                L.r.inv = rtv::V3{rtd::rcp_ieee(b.x), rtd::rcp_ieee(b.y), rtd::rcp_ieee(b.z)};   // Ray::inv, exactly
+                L.T.a = __float_as_uint(a.w);
+                L.T.b = __float_as_uint(b.w);
+                L.T.best = rtd::Hit{c.x, c.y, c.z, __float_as_int(c.w)};
+                L.T.acc = d.x;
+                L.T.sp = (int)(__float_as_uint(d.y) & 255u);
+                L.T.phase = (int)(__float_as_uint(d.y) >> 8);
+            }
         } else {
             rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
                                                                                root, S, nodes, cnt, kSpec && tail);
@@ -472,6 +506,16 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #define RT_POOL_PARK 1
 #endif
 constexpr bool kPoolPark = RT_POOL_PARK != 0;
+// RT_POOL_DEFER_HIT: a finished traversal's hit store waits for the next step's loads (above).
+#ifndef RT_POOL_DEFER_HIT
+#define RT_POOL_DEFER_HIT 1
+#endif
+constexpr bool kPoolDeferHit = RT_POOL_DEFER_HIT != 0;
+// RT_POOL_HITLDS: hits of ready paths in LDS by ready-ring position (below); 0: in the record.
+#ifndef RT_POOL_HITLDS
+#define RT_POOL_HITLDS 1
+#endif
+constexpr bool kPoolHitLds = RT_POOL_HITLDS != 0;
 template <bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMegaWpe, 8)))
 rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
@@ -480,6 +524,10 @@ rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ float lut[256];
     __shared__ uint8_t ring_q[4][rtd::kPool], ring_r[4][rtd::kPool];
+    // hits of ready paths by ready-ring position (mod 64): a finished traversal's hit goes to
+    // LDS, not to the path record, so the traversal loop issues no global store (a store would
+    // make the next step's load waits wait for it too: vmcnt counts both)
+    __shared__ float4 hit_slot[4][64];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) lut[k] = sc_in.lut[k];
     __syncthreads();
     DevScene sc = sc_in;
@@ -497,16 +545,59 @@ rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     for (int q = 0; q < rtd::kPoolPerLane; ++q) {   // every path of the pool takes a pixel
         const int j = lane + 64 * q;
         const int pix = rtd::pool_claim(true, queue, n_items, order, exhausted);
-        if (pix >= 0) rtd::pool_assign(V, wbase + j, sc, g, pix, root);
-        rtd::pool_push(rq, qt, pix >= 0, j);
+        const int nx = pix >= 0 ? rtd::pool_assign<COUNT>(V, wbase + j, sc, g, pix, root, cnt) : rtd::PN_PIXEL;
+        rtd::pool_push(rq, qt, nx == rtd::PN_QUEUE, j);
+        rtd::pool_push(rr, rt, nx == rtd::PN_READY, j);
     }
-    rtd::Ray r;
-    rtd::TravStateU T;
+    rtd::Ray r{};
+    rtd::TravStateU T;   // (defined for every lane: a free lane's state is parked too)
+    T.a = T.b = 0u;
+    T.acc = 1e9f;
+    T.sp = 0;
+    T.phase = rtd::TP_POP;
+    T.best = rtd::Hit{1e9f, 0.f, 0.f, -1};
     int jc = 0;          // the path this lane traverses (number in the pool)
     bool trav = false;
-    // a traversal that has ended (done): its hit to the path record, the path to the ready ring
+    // A traversal that has ended (done): the path goes to the ready ring at once, its hit to the
+    // path record one step later (pend / ph / pj), by the next step's hook, after that step's
+    // loads have arrived: a store issued before them would make their waits wait for it too
+    // (vmcnt).  Every pending hit is stored before a shading pass reads it (flush).
+    bool pend = false;
+    int pj = 0;
+    rtd::Hit ph{1e9f, 0.f, 0.f, -1};
+    auto flush = [&]() {
+        if (pend) rtd::pool_st(V.C(wbase + pj), make_float4(ph.t, ph.u, ph.v, __int_as_float(ph.prim)));
+        pend = false;
+    };
     auto finish = [&](bool done) {
-        if (done) *V.C(wbase + jc) = make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
+        if constexpr (kPoolHitLds) {
+            // ready-ring entry: path number, bit 7 = the hit is in LDS slot (position % 64); free
+            // unless 64 or more ready paths are ahead of it (then the path record, as below)
+            const unsigned long long m = __ballot(done);
+            if (m) {
+                const int pos = rt + __popcll(m & ((1ull << lane) - 1ull));
+                const bool in_lds = pos - rh < 64;
+                if (done && in_lds)
+                    hit_slot[wave][pos & 63] =
+                        make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
+                if (done && !in_lds)
+                    rtd::pool_st(V.C(wbase + jc), make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim)));
+                if (done) rr[(unsigned)pos % (unsigned)rtd::kPool] = (uint8_t)(jc | (in_lds ? 0x80 : 0));
+                rt += __popcll(m);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+            return;
+        }
+        if (done) {
+            if constexpr (kPoolDeferHit) {
+                pend = true;
+                pj = jc;
+                ph = T.best;
+            } else {
+                rtd::pool_st(V.C(wbase + jc), make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim)));
+            }
+        }
         rtd::pool_push(rr, rt, done, jc);
     };
     // free lanes take queued paths (ring order)
@@ -516,39 +607,66 @@ rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         const int take = nf < nq ? nf : nq;
         if (take <= 0) return;
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-        bool done = false;
         if (!trav && rank < take) {
             jc = rq[(unsigned)(qh + rank) % (unsigned)rtd::kPool];
-            uint32_t miss;
-            r = rtd::pool_load_ray(V, wbase + jc, miss);
-            trav = rtd::trav_start<COUNT>(miss ? 8u : 0u, root.a, root.b, T, cnt);
-            done = !trav;   // the ray misses the scene box: no hit
+            r = rtd::pool_load_ray(V, wbase + jc);
+            trav = rtd::trav_start<COUNT>(0u, root.a, root.b, T, cnt);   // (queued rays enter the root box)
         }
         qh += take;
-        finish(done);
     };
+#ifdef RT_MEGA_PROF
+    // (diagnostics build: the lane-resident kernel's g_mega_prof slots, same meaning)
+    unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
+    __syncthreads();
+    long long tp = clock64();
+    const unsigned long long wt0 = wall_clock64();
+#endif
     for (;;) {
         refill();
         const int nt = __popcll(__ballot(trav)), nready = rt - rh;
         if (nt == 0 && nready == 0) break;   // (the refill emptied the queue: every path has retired)
+#ifdef RT_MEGA_PROF
+        {
+            const long long t1 = clock64();
+            pf[2] += (unsigned long long)(t1 - tp);
+            tp = t1;
+        }
+#endif
         if (nt > 0 && nready < rtd::kPoolBatch) {
             // traversal iterations until kPoolBatch paths are ready or no lane traverses; free
             // lanes are refilled in batches of kPoolRefill
             int kt = nt;
             do {
+#ifdef RT_MEGA_PROF
+                pf[4] += 1;
+                pf[6] += (unsigned long long)kt;
+#endif
                 const bool done = rtd::trav_step_coop<COUNT, kCoopLeavesPlain>(sc, r, T, S, nodes, cnt, trav,
-                                                                               kCoopRoundMinPlain);
+                                                                               kCoopRoundMinPlain, flush);
                 if (done) trav = false;
                 finish(done);
                 if (__popcll(__ballot(!trav)) >= rtd::kPoolRefill && qt > qh) refill();
                 kt = __popcll(__ballot(trav));
             } while (kt > 0 && rt - rh < rtd::kPoolBatch);
+            flush();
+#ifdef RT_MEGA_PROF
+            {
+                const long long t1 = clock64();
+                pf[1] += (unsigned long long)(t1 - tp);
+                tp = t1;
+            }
+#endif
             continue;
         }
+#ifdef RT_MEGA_PROF
+        pf[3] += 1;
+        pf[5] += (unsigned long long)(nready < 64 ? nready : 64);
+#endif
         // shading pass: lanes 0..ns-1 shade the oldest ready paths; a lane that traverses
         // another path keeps its frames, the light walk stacks above them
         const int ns = nready < 64 ? nready : 64;
-        bool push = false, need = false;
+        int nx = rtd::PN_PIXEL;
         int js = 0;
         const int sp0 = trav ? T.sp : 0;
         if constexpr (kPoolPark) {
@@ -558,14 +676,19 @@ rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             {
                 const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
                 st.st[2 * slot] = make_float4(__uint_as_float(T.a), __uint_as_float(T.b), T.acc,
-                                              __uint_as_float((uint32_t)T.sp | (uint32_t)T.phase << 8 | (uint32_t)jc << 16));
+                                              __uint_as_float(((uint32_t)T.sp & 255u) | ((uint32_t)T.phase & 255u) << 8 |
+                                                              ((uint32_t)jc & 255u) << 16));
                 st.st[2 * slot + 1] = make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
             }
         }
         if (lane < ns) {
-            js = rr[(unsigned)(rh + lane) % (unsigned)rtd::kPool];
+            const int pos = rh + lane;
+            js = rr[(unsigned)pos % (unsigned)rtd::kPool];
+            const bool in_lds = kPoolHitLds && (js & 0x80);
+            js &= 0x7f;
+            const float4 h4 = in_lds ? hit_slot[wave][pos & 63] : rtd::pool_ld(V.C(wbase + js));
             rtd::OffsetStack<decltype(S)> os{S, sp0};
-            need = rtd::pool_shade<COUNT>(V, wbase + js, sc, g, st, spp, out, root, os, cnt, push);
+            nx = rtd::pool_shade<COUNT>(V, wbase + js, h4, sc, g, st, spp, out, root, os, cnt);
         }
         if constexpr (kPoolPark) {
             {
@@ -577,17 +700,39 @@ rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 T.acc = a.z;
                 T.sp = (int)(w & 255u);
                 T.phase = (int)((w >> 8) & 255u);
-                jc = (int)(w >> 16);
+                jc = (int)((w >> 16) & 255u);
                 T.best = rtd::Hit{b.x, b.y, b.z, __float_as_int(b.w)};
-                uint32_t miss;
-                r = rtd::pool_load_ray(V, wbase + jc, miss);
+                r = rtd::pool_load_ray(V, wbase + jc);
             }
         }
         rh += ns;
-        const int pix = rtd::pool_claim(need, queue, n_items, order, exhausted);
-        if (pix >= 0) rtd::pool_assign(V, wbase + js, sc, g, pix, root);
-        rtd::pool_push(rq, qt, push || pix >= 0, js);
+        {   // paths whose pixel is done take the next pixel (or retire)
+            const int pix = rtd::pool_claim(lane < ns && nx == rtd::PN_PIXEL, queue, n_items, order, exhausted);
+            if (pix >= 0) nx = rtd::pool_assign<COUNT>(V, wbase + js, sc, g, pix, root, cnt);
+        }
+        rtd::pool_push(rq, qt, lane < ns && nx == rtd::PN_QUEUE, js);
+        rtd::pool_push(rr, rt, lane < ns && nx == rtd::PN_READY, js);
+#ifdef RT_MEGA_PROF
+        {
+            const long long t1 = clock64();
+            pf[0] += (unsigned long long)(t1 - tp);
+            tp = t1;
+        }
+#endif
     }
+#ifdef RT_MEGA_PROF
+    if (lane == 0) {
+        for (int k = 0; k < 7; ++k) atomicAdd(&g_mega_prof[k], pf[k]);
+        atomicAdd(&g_mega_prof[7], 1ull);
+        const unsigned wi = atomicAdd(&g_wave_n, 1u);
+        if (wi < (unsigned)kProfWaves) {
+            g_wave_t[2 * wi] = wt0;
+            g_wave_t[2 * wi + 1] = wall_clock64();
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
+#endif
     rtd::counters_flush<COUNT>(cnt, counters);
 }
 
@@ -1254,6 +1399,9 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const unsigned blocks = pool ? persistent_blocks(d, pk, (n_items + rtd::kPoolPerLane - 1) / rtd::kPoolPerLane)
                                          : persistent_blocks(d, mk, n_items * kClaimStride);
             const long long slots = (long long)blocks * 256 * (pool ? rtd::kPoolPerLane : 1);   // lane slots / paths
+            // records and pool planes are addressed with 32-bit byte offsets (rt_path.h LaneRec)
+            if ((unsigned long long)slots * (unsigned long long)s->ray_depth * 32ull >= (1ull << 32))
+                return rt_fail(RT_ERR_LIMIT, "rt_render: vertex records beyond 4 GiB");
             int rc = ensure_wf(d, std::max<long long>(g.n_pixels, slots), s->ray_depth);   // vertex records
             if (rc) return rc;
             rtd::WfState w = d->wf;

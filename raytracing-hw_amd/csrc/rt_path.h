@@ -736,6 +736,31 @@ struct AosRec {
 // marks (coeff = 1 / pdf > 0, so the bit is free).  Round 2 kept (e, coeff), (m, cos) and
 // alpha in three planes: each vertex touched three sectors, and the records were 79% of
 // the kernel's HBM writes (profiles/r02e_record_layout_ab.jsonl).
+// Record addresses are a uniform base plus a 32-bit byte offset (lanes x depth x 32 B stays
+// below 4 GiB: the host sizes the workspace), so a record access is one VGPR of offset on the
+// base in SGPRs rather than a 64-bit address per lane.
+// RT_REC_NT (A/B builds): the vertex records written and read back non-temporally.
+#ifndef RT_REC_NT
+#define RT_REC_NT 0
+#endif
+__device__ __forceinline__ void rec_st(float4 &dst, float4 v) {
+#if RT_REC_NT && defined(__HIP_DEVICE_COMPILE__)
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4f *>(&dst));
+#else
+    dst = v;
+#endif
+}
+__device__ __forceinline__ float4 rec_ld(const float4 &src) {
+#if RT_REC_NT && defined(__HIP_DEVICE_COMPILE__)
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f x = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(&src));
+    return make_float4(x.x, x.y, x.z, x.w);
+#else
+    return src;
+#endif
+}
 struct LaneRec {
     float4 *R;
     float *al;
@@ -743,20 +768,24 @@ struct LaneRec {
     V3 e;
     int ek;
     bool pending;
-    __device__ __forceinline__ long long v(int k) const { return (long long)k * lanes + i; }
+    __device__ __forceinline__ uint32_t v(int k) const { return (uint32_t)k * (uint32_t)lanes + (uint32_t)i; }
+    __device__ __forceinline__ float4 &rec(uint32_t vk, int half) const {
+        return *(float4 *)((char *)R + (size_t)((vk << 5) + (uint32_t)(16 * half)));
+    }
+    __device__ __forceinline__ float &alp(uint32_t vk) const { return *(float *)((char *)al + (size_t)(vk << 2)); }
     __device__ __forceinline__ void set_e(int k, V3 x) { e = x; ek = k; pending = true; }
     __device__ __forceinline__ void set_brdf(int k, V3 mm, float cf, float cs, float a) {
         const bool one = __float_as_uint(a) == 0x3f800000u;
-        R[2 * v(k)] = make_float4(__uint_as_float(__float_as_uint(cf) | (one ? 0u : 0x80000000u)), mm.x, mm.y, mm.z);
-        R[2 * v(k) + 1] = make_float4(cs, e.x, e.y, e.z);
-        if (!one) al[v(k)] = a;
+        rec_st(rec(v(k), 0), make_float4(__uint_as_float(__float_as_uint(cf) | (one ? 0u : 0x80000000u)), mm.x, mm.y, mm.z));
+        rec_st(rec(v(k), 1), make_float4(cs, e.x, e.y, e.z));
+        if (!one) alp(v(k)) = a;
         pending = false;
     }
     __device__ __forceinline__ void flush_e() {
-        if (pending) R[2 * v(ek) + 1] = make_float4(0.f, e.x, e.y, e.z);
+        if (pending) rec_st(rec(v(ek), 1), make_float4(0.f, e.x, e.y, e.z));
         pending = false;
     }
-    __device__ __forceinline__ V3 get_e(int k) const { const float4 b = R[2 * v(k) + 1]; return V3{b.y, b.z, b.w}; }
+    __device__ __forceinline__ V3 get_e(int k) const { const float4 b = rec_ld(rec(v(k), 1)); return V3{b.y, b.z, b.w}; }
 };
 // fold_path over LaneRec: the backward recurrence, records read four vertices at a time
 // (alpha only for the vertices that stored one).  last_here: the last vertex was shaded in
@@ -765,7 +794,7 @@ __device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv, bool last_here
     if (nv == 0) return V3{0.f, 0.f, 0.f};
     V3 c = P.e;
     if (!last_here) {
-        const float4 last = P.R[2 * P.v(nv - 1) + 1];
+        const float4 last = rec_ld(P.rec(P.v(nv - 1), 1));
         c = V3{last.y, last.z, last.w};
     }
     for (int hi = nv - 2; hi >= 0; hi -= 4) {
@@ -773,14 +802,14 @@ __device__ __forceinline__ V3 fold_path(const LaneRec &P, int nv, bool last_here
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int k = hi - j >= 0 ? hi - j : 0;
-            A[j] = P.R[2 * P.v(k)];
-            B[j] = P.R[2 * P.v(k) + 1];
+            A[j] = rec_ld(P.rec(P.v(k), 0));
+            B[j] = rec_ld(P.rec(P.v(k), 1));
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (hi - j < 0) break;
             const uint32_t cb = __float_as_uint(A[j].x);
-            const float alpha = (cb >> 31) ? P.al[P.v(hi - j)] : 1.f;
+            const float alpha = (cb >> 31) ? P.alp(P.v(hi - j)) : 1.f;
             V3 x = rtv::mul(c, __uint_as_float(cb & 0x7fffffffu));
             x = rtv::mulv(x, V3{A[j].y, A[j].z, A[j].w});
             x = rtv::mul(x, B[j].x);

@@ -599,9 +599,17 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
 // round per step).  A wave mostly at leaves (a scene of a few dozen triangles, whose tree
 // is a few levels deep) otherwise serves kCoopLeaves of its leaf lanes per step and idles
 // the rest (rt_device.hip kCoopRoundMin*).
-template <bool COUNT, int kCoopLeaves, class Stack, class Nodes, class TS>
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+// hook: called by every lane once the step's loads have all arrived (after the leaf rounds,
+// before the node test): the pool kernel issues its previous step's hit store there, so that
+// no wait of this step's loads also waits for that store (vmcnt counts loads and stores in
+// issue order).
+template <bool COUNT, int kCoopLeaves, class Stack, class Nodes, class TS, class Hook = NoHook>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TS &T, Stack &stk,
-                                               const Nodes &nodes, Counters &cnt, bool active, int round_min) {
+                                               const Nodes &nodes, Counters &cnt, bool active, int round_min,
+                                               const Hook &hook = Hook{}) {
     static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
     __shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)
     const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
@@ -691,6 +699,7 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
             if (T.k >= T.kend) T.phase = TP_POP;
         }
     }
+    hook();
     // node lanes: the pair test
     if (at_node) node_step<COUNT>(q, r, T, stk, cnt);
     if (active && T.phase == TP_POP) return trav_pop(T, stk);
