@@ -2026,9 +2026,23 @@ void coop_cases(std::vector<float> &tri, std::vector<float> &rays, std::vector<u
 
 extern "C" {
 
+// rt_device_selfcheck 3: the traversal's box-distance root (rt_wavefront.h sqrt_cr) against
+// the IEEE sqrtf over every float (NaN results compared as NaN).
+__global__ void __launch_bounds__(256) sqrt_check_kernel(unsigned long long *bad) {
+    unsigned long long local = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float x = __uint_as_float((uint32_t)i);
+        const float a = rtd::sqrt_cr(x), b = sqrtf(x);
+        local += (isnan(a) && isnan(b)) ? 0ull : (__float_as_uint(a) != __float_as_uint(b) ? 1ull : 0ull);
+    }
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
+}
+
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
     if (!mismatches) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: null output");
-    if (which < 0 || which > 2) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
+    if (which < 0 || which > 3) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
     unsigned long long *d = nullptr;
     HIP_TRY(hipMalloc((void **)&d, sizeof *d));
     hipError_t e = hipMemset(d, 0, sizeof *d);
@@ -2036,6 +2050,8 @@ int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
     if (e == hipSuccess) {
         if (which == 0) {
             hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
+        } else if (which == 3) {
+            hipLaunchKernelGGL(sqrt_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
         } else if (which == 1) {
             hipLaunchKernelGGL(decode_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
         } else {

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/pool_ab.py --steps 3 --worlds 1 --modes lane --libs raytracing-hw_amd/librt_hw_amd.so,raytracing-hw_amd/v_park_off/librt_hw_amd.so > gpurun_out/r04f_park_ab.jsonl 2>&1 || { tail -5 gpurun_out/r04f_park_ab.jsonl; exit 1; }
+timeout -k 10 300 python -u tools/pool_ab.py --steps 3 --worlds 1 --modes lane --libs raytracing-hw_amd/librt_hw_amd.so,raytracing-hw_amd/v_park_off/librt_hw_amd.so,raytracing-hw_amd/v_sqrt_off/librt_hw_amd.so,raytracing-hw_amd/v_base3/librt_hw_amd.so > gpurun_out/r04f_park_ab.jsonl 2>&1 || { tail -5 gpurun_out/r04f_park_ab.jsonl; exit 1; }
 cat gpurun_out/r04f_park_ab.jsonl | grep '^{'
 WORLDS=8 timeout -k 10 400 bash tools/runahead_variants.sh default raytracing-hw_amd/v_t8w6/librt_hw_amd.so raytracing-hw_amd/v_t4w8/librt_hw_amd.so raytracing-hw_amd/v_t16w5/librt_hw_amd.so raytracing-hw_amd/v_t2w10/librt_hw_amd.so || exit 1
 cp gpurun_out/runahead_variants.jsonl gpurun_out/r04f_tail_ab.jsonl
