@@ -233,9 +233,8 @@ int rt_device_synchronize(void);
  * (float)b / 255.f for every byte, and the packed LDS RNG word round trip over every minstd
  * state and both normal-cache flags; which 2: the cooperative leaf step (rt_wavefront.h
  * trav_step_coop) against the per-lane in-order strict-< loop over 2^16 synthetic leaves rich
- * in equal-t ties, NaN and infinite vertices (four launches); which 3: the traversal's box
- * distance root (rt_wavefront.h sqrt_cr) against sqrtf over every float; *mismatches =
- * values (cases) that differ (0 = exact). */
+ * in equal-t ties, NaN and infinite vertices (four launches); *mismatches = values (cases)
+ * that differ (0 = exact). */
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches);
 
 #ifdef __cplusplus

@@ -80,12 +80,6 @@ constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #define RT_PLAIN_TRAV_SHARED 1
 #endif
 constexpr bool kPlainTravShared = RT_PLAIN_TRAV_SHARED != 0;
-// The lane-resident kernel parks its lanes' traversal state in memory around a shading pass
-// (rt_mega_kernel); 0: kept in registers (the compiler spills it), for A/B builds.
-#ifndef RT_PARK_TRAV
-#define RT_PARK_TRAV 1
-#endif
-constexpr bool kParkTrav = RT_PARK_TRAV != 0;
 // ... whose leaf work is spread over the wave (rt_wavefront.h trav_step_coop).  0: per-lane
 // leaf steps of RT_LEAF_N triangles, for A/B builds.
 #ifndef RT_COOP_LEAF
@@ -438,34 +432,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 pf[6] += (unsigned long long)kt;
 #endif
             } while (true);
-        } else if (kParkTrav && !kSpec && !LSPLIT && shade_now) {
-            // Shading pass with the traversal state parked: every lane stores its ray and
-            // traversal state to its lane slot of WfState::mid before the pass, and a lane that
-            // did not start a new ray in the pass (it was traversing, or went idle) reloads it
-            // after, so none of it is live across the shading code (which the compiler would
-            // otherwise spill and reload around the pass and at the loop's back-edge).
-            const long long slot = rtd::mega_slot(), ln = st.lanes;
-            float4 *pk = st.mid;
-            pk[slot] = make_float4(L.r.o.x, L.r.o.y, L.r.o.z, __uint_as_float(L.T.a));
-            pk[ln + slot] = make_float4(L.r.d.x, L.r.d.y, L.r.d.z, __uint_as_float(L.T.b));
-            pk[2 * ln + slot] = make_float4(L.T.best.t, L.T.best.u, L.T.best.v, __int_as_float(L.T.best.prim));
-            pk[3 * ln + slot] = make_float4(L.T.acc, __uint_as_float((uint32_t)L.T.sp | (uint32_t)L.T.phase << 8), 0.f, 0.f);
-            const bool was_ready = L.state == rtd::M_READY;
-            rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, true, sc, g, st, spp, out, cost,
-                                                                               root, S, nodes, cnt, false);
-            const bool fresh = was_ready && (L.state == rtd::M_TRAV || L.state == rtd::M_READY);   // a new ray
-            if (!fresh) {
-                const float4 a = pk[slot], b = pk[ln + slot], c = pk[2 * ln + slot], d = pk[3 * ln + slot];
-                L.r.o = rtv::V3{a.x, a.y, a.z};
-                L.r.d = rtv::V3{b.x, b.y, b.z};
-                L.r.inv = rtv::V3{rtd::rcp_ieee(b.x), rtd::rcp_ieee(b.y), rtd::rcp_ieee(b.z)};   // Ray::inv, exactly
-                L.T.a = __float_as_uint(a.w);
-                L.T.b = __float_as_uint(b.w);
-                L.T.best = rtd::Hit{c.x, c.y, c.z, __float_as_int(c.w)};
-                L.T.acc = d.x;
-                L.T.sp = (int)(__float_as_uint(d.y) & 255u);
-                L.T.phase = (int)(__float_as_uint(d.y) >> 8);
-            }
         } else {
             rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
                                                                                root, S, nodes, cnt, kSpec && tail);
@@ -2026,23 +1992,9 @@ void coop_cases(std::vector<float> &tri, std::vector<float> &rays, std::vector<u
 
 extern "C" {
 
-// rt_device_selfcheck 3: the traversal's box-distance root (rt_wavefront.h sqrt_cr) against
-// the IEEE sqrtf over every float (NaN results compared as NaN).
-__global__ void __launch_bounds__(256) sqrt_check_kernel(unsigned long long *bad) {
-    unsigned long long local = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32);
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const float x = __uint_as_float((uint32_t)i);
-        const float a = rtd::sqrt_cr(x), b = sqrtf(x);
-        local += (isnan(a) && isnan(b)) ? 0ull : (__float_as_uint(a) != __float_as_uint(b) ? 1ull : 0ull);
-    }
-    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
-    if ((threadIdx.x & 63) == 0 && local) atomicAdd(bad, local);
-}
-
 int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
     if (!mismatches) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: null output");
-    if (which < 0 || which > 3) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
+    if (which < 0 || which > 2) return rt_fail(RT_ERR_ARG, "rt_device_selfcheck: unknown check " + std::to_string(which));
     unsigned long long *d = nullptr;
     HIP_TRY(hipMalloc((void **)&d, sizeof *d));
     hipError_t e = hipMemset(d, 0, sizeof *d);
@@ -2050,8 +2002,6 @@ int rt_device_selfcheck(int32_t which, uint64_t *mismatches) {
     if (e == hipSuccess) {
         if (which == 0) {
             hipLaunchKernelGGL(rcp_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
-        } else if (which == 3) {
-            hipLaunchKernelGGL(sqrt_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
         } else if (which == 1) {
             hipLaunchKernelGGL(decode_check_kernel, dim3(4096), dim3(256), 0, nullptr, d);
         } else {

@@ -146,41 +146,12 @@ __device__ __forceinline__ bool box_hit_pt(const float mn[3], const float mx[3],
     inside_out = inside;
     return inside || !out;
 }
-// sqrtf, correctly rounded, without the compiler's range handling where it is not needed:
-// the hardware root (within 1 ulp) and the residual test of its two neighbours, which is the
-// IEEE root for every finite x >= 2^-96 (the compiler's own expansion scales x below 2^-96 and
-// passes 0, inf and NaN through; those take the library sqrtf in a branch no box distance of a
-// real scene reaches).  Checked against sqrtf over every float on the device
-// (rt_device_selfcheck 3).  The host build calls sqrtf.
-#ifndef RT_SQRT_CR
-#define RT_SQRT_CR 1   // 0: the compiler's sqrtf expansion (A/B builds)
-#endif
-__device__ __forceinline__ float sqrt_cr(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SQRT_CR
-    const bool fast = (x >= 0x1p-96f) & (x <= 0x1.fffffep+127f);
-    const float xf = fast ? x : 1.f;
-    const float s0 = __builtin_amdgcn_sqrtf(xf);
-    const float sdn = __uint_as_float(__float_as_uint(s0) - 1u), sup = __uint_as_float(__float_as_uint(s0) + 1u);
-    const float rdn = __builtin_fmaf(-sdn, s0, xf), rup = __builtin_fmaf(-sup, s0, xf);
-    float s = rdn <= 0.f ? sdn : s0;
-    s = rup > 0.f ? sup : s;
-    if (__builtin_expect(!fast, 0)) s = sqrtf(x);
-    return s;
-#else
-    return sqrtf(x);
-#endif
-}
-
-// Entry distance of a box from box_hit_pt's results (0 from inside): rtv::length of
-// (coord - origin), the same products and sums, its root by sqrt_cr (an inside lane's value is
-// not used, so it feeds 1 and never takes sqrt_cr's slow branch).
+// Entry distance of a box from box_hit_pt's results (0 from inside).  (Round 4: the root as
+// the hardware sqrt plus the residual correction, without the compiler's scaling and class
+// handling, and a branch to sqrtf outside [2^-96, max]: exact over every float, but 1143 vs
+// 1136 ms: the branch costs more than the selects it saves; profiles/r04f_park_sqrt_ab.jsonl.)
 __device__ __forceinline__ float box_dist(const float coord[3], bool inside, const Ray &r) {
-    const V3 d = rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o);
-    float m = 0.f;
-    m += d.x * d.x;
-    m += d.y * d.y;
-    m += d.z * d.z;
-    const float l = sqrt_cr(inside ? 1.f : m);
+    const float l = rtv::length(rtv::sub(V3{coord[0], coord[1], coord[2]}, r.o));
     return inside ? 0.f : l;
 }
 template <bool DIST>

@@ -394,13 +394,6 @@ def test_coop_leaf_step_ties_and_nan(gpu):
     assert gpu.device_selfcheck(2) == 0
 
 
-def test_box_distance_root_is_exact(gpu):
-    """The node step's entry-distance root (rt_wavefront.h sqrt_cr: the hardware root and one
-    residual correction, the library sqrtf below 2^-96 and for 0, inf, NaN) equals sqrtf for
-    every float on the device (rt_device_selfcheck 3)."""
-    assert gpu.device_selfcheck(3) == 0
-
-
 def test_schedule_reported(gpu):
     """rt_stats.schedule names the kernel that rendered: the plain lane-resident kernel for a
     frame of more pixels than lanes (or a counting render), the runahead kernel for its 8-way
