@@ -129,10 +129,6 @@ typedef struct {
  * runahead): same bits, shorter frame tail.  This flag turns it off.  (Counting renders,
  * count = 1, never use it: their counters are those of the sequential chain.) */
 #define RT_FLAG_NO_RUNAHEAD 16
-/* Path-pool schedule (rt_pool.h; parity mode, shards of more than 2 pixels per lane): each
- * wave keeps 64 x 2 paths in HBM and its lanes traverse whichever path is queued, so no lane
- * waits for a shading batch.  Same bits. */
-#define RT_FLAG_POOL 64
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */
@@ -164,7 +160,6 @@ typedef struct {
 #define RT_SCHED_FAST 4         /* fast mode (RT_FLAG_FAST)                                 */
 #define RT_SCHED_LIGHT_SPLIT 8  /* light-split kernel (RT_FLAG_LIGHT_SPLIT)                 */
 #define RT_SCHED_WAVEFRONT 16   /* wavefront launches (RT_KERNEL_WAVEFRONT)                 */
-#define RT_SCHED_POOL 32        /* path-pool schedule of the lane-resident kernel (rt_pool.h) */
 
 /* --- scene ------------------------------------------------------------------------ */
 int rt_scene_load_gltf(const char *path, int32_t width, int32_t height, int32_t samples, rt_scene **out);

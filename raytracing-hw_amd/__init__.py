@@ -54,8 +54,7 @@ FLAG_NATURAL_ORDER = 8   # RT_FLAG_NATURAL_ORDER: row-major pixel order instead 
 FLAG_NO_RUNAHEAD = 16    # RT_FLAG_NO_RUNAHEAD: no speculative sample runahead in the waves' tails (same bits)
 FLAG_HEAVY_ORDER = 32    # RT_FLAG_HEAVY_ORDER: the heaviest-first order below 128 spp too (same bits)
 # RtStats.schedule bits (include/rt_hw.h RT_SCHED_*): the kernels that rendered
-SCHED_LANE, SCHED_RUNAHEAD, SCHED_FAST, SCHED_LIGHT_SPLIT, SCHED_WAVEFRONT, SCHED_POOL = 1, 2, 4, 8, 16, 32
-FLAG_POOL = 64           # RT_FLAG_POOL: path-pool schedule (rt_pool.h; same bits)
+SCHED_LANE, SCHED_RUNAHEAD, SCHED_FAST, SCHED_LIGHT_SPLIT, SCHED_WAVEFRONT = 1, 2, 4, 8, 16
 
 
 class RtParams(ctypes.Structure):
@@ -220,15 +219,14 @@ class Scene:
         _check(lib().rt_scene_upload(self._h, device))
 
     def _params(self, spp, rank, world, row_block, count, kernel, kernel_times=False, fast=False, fast_chunk=0,
-                device=0, light_split=False, natural_order=False, runahead=True, heavy_order=False, pool=False):
+                device=0, light_split=False, natural_order=False, runahead=True, heavy_order=False):
         flags = ((FLAG_KERNEL_TIMES if kernel_times else 0) | (FLAG_FAST if fast else 0) |
                  (FLAG_LIGHT_SPLIT if light_split else 0) | (FLAG_NATURAL_ORDER if natural_order else 0) |
-                 (0 if runahead else FLAG_NO_RUNAHEAD) | (FLAG_HEAVY_ORDER if heavy_order else 0) |
-                 (FLAG_POOL if pool else 0))
+                 (0 if runahead else FLAG_NO_RUNAHEAD) | (FLAG_HEAVY_ORDER if heavy_order else 0))
         return RtParams(spp or 0, rank, world, row_block, int(count), kernel, flags, fast_chunk, device)
 
     def render_sums(self, spp=None, rank=0, world=1, row_block=8, count=False, kernel=0, device=0, fast=False,
-                    fast_chunk=0, light_split=False, natural_order=False, runahead=True, heavy_order=False, pool=False):
+                    fast_chunk=0, light_split=False, natural_order=False, runahead=True, heavy_order=False):
         """Per-pixel float RGB sums of the owned rows (sample_canvas, scene.cpp:20,42).
         fast=True: fast mode (RT_FLAG_FAST, work units of fast_chunk samples): statistically
         equivalent to the reference, not bit-identical.  light_split / natural_order /
@@ -239,7 +237,7 @@ class Scene:
         st = RtStats()
         p = self._params(spp, rank, world, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk, device=device,
                          light_split=light_split, natural_order=natural_order, runahead=runahead,
-                         heavy_order=heavy_order, pool=pool)
+                         heavy_order=heavy_order)
         _check(lib().rt_render(self._h, ctypes.byref(p), out.ctypes.data_as(_c_f), ctypes.byref(st)))
         return out, st.as_dict()
 
@@ -276,12 +274,12 @@ class Scene:
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
                       kernel=0, stats=False, kernel_times=False, fast=False, fast_chunk=0, device=0,
-                      light_split=False, natural_order=False, runahead=True, heavy_order=False, pool=False):
+                      light_split=False, natural_order=False, runahead=True, heavy_order=False):
         """Launch into device memory (e.g. a torch tensor's data_ptr()) on a HIP stream, on
         `device` (upload(device) first).  kernel_times: per-launch HIP-event timing of the
         wavefront kernels (needs stats).  fast: fast mode (RT_FLAG_FAST), see render_sums."""
         p = self._params(spp, rank, world, row_block, count, kernel, kernel_times, fast, fast_chunk, device,
-                         light_split, natural_order, runahead, heavy_order, pool)
+                         light_split, natural_order, runahead, heavy_order)
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))

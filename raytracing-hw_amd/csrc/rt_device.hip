@@ -32,7 +32,6 @@
 #include "rt_wavefront.h"
 #include <type_traits>
 #include "rt_mega.h"
-#include "rt_pool.h"
 #include "rt_quant_lut.h"
 #include "rt_scene.h"
 #include "rt_bvh_layout.h"
@@ -98,6 +97,12 @@ constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
 #define RT_SPEC_COOP_LEAVES 16
 #endif
 constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // the runahead kernel's coop leaf records per wave
+// The runahead kernel's coop step issues the child-pair loads from node lanes only
+// (rt_wavefront.h trav_step_coop MASK_LOAD; the plain kernel measured slower with it).
+#ifndef RT_SPEC_MASK_LOAD
+#define RT_SPEC_MASK_LOAD 1
+#endif
+constexpr bool kSpecMaskLoad = RT_SPEC_MASK_LOAD != 0;
 // Leaf rounds per coop step (rt_wavefront.h trav_step_coop round_min): a further round
 // while at least this many leaf lanes are unserved.  Plain kernel: 8 (sponza 1080p 1292 ->
 // 1278 ms against one round per step).  Runahead kernel: 4 on scenes of fewer than
@@ -145,6 +150,14 @@ constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units 
 #define RT_SPEC_PIXELS_PER_LANE 2
 #endif
 constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
+// Runahead kernel launched on every resident block (RT_SPEC_FILL=1), not just ceil(pixels / 256):
+// a wave's first claim takes at most ceil(pixels / waves) pixels, so where a shard has fewer
+// pixels than resident lanes (an 8-way shard at 5 waves per SIMD) every wave starts with idle
+// lanes for runahead.  0: one lane per pixel, ceil(pixels / 256) blocks.
+#ifndef RT_SPEC_FILL
+#define RT_SPEC_FILL 0
+#endif
+constexpr bool kSpecFill = RT_SPEC_FILL != 0;
 // Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
 // holds at most 64 / k pixels and the grid grows k-fold (lockstep study).
 #ifndef RT_CLAIM_STRIDE
@@ -328,6 +341,15 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     L.state = rtd::M_IDLE;
     bool exhausted = false;
     bool tail = false, wave_room = false;
+    // RT_SPEC_FILL: wave w takes queue items [w * quota, (w + 1) * quota) on lanes 0 .. quota-1
+    // (quota = ceil(items / waves), so every item is assigned at once) and no queue is claimed
+    if constexpr (kSpec && kSpecFill) {
+        const long long waves = 4LL * gridDim.x, q = (n_items + waves - 1) / waves;
+        const int quota = q < 64 ? (int)q : 64;
+        const long long p = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * quota + lane;
+        if (q <= 64 && lane < quota && p < n_items) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
+        exhausted = q <= 64;   // (more items than lanes: the queue hands out the rest)
+    }
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -417,7 +439,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             int kt = nt;
             do {
                 if (kCoopLeaf) {
-                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain>(
+                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain, kSpec && kSpecMaskLoad>(
                             sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV,
                             kSpec ? st.round_min : kCoopRoundMinPlain))
                         L.state = rtd::M_READY;
@@ -440,248 +462,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         {
             const long long t1 = clock64();
             pf[shade_now ? 0 : 1] += (unsigned long long)(t1 - tp);
-            tp = t1;
-        }
-#endif
-    }
-#ifdef RT_MEGA_PROF
-    if (lane == 0) {
-        for (int k = 0; k < 7; ++k) atomicAdd(&g_mega_prof[k], pf[k]);
-        atomicAdd(&g_mega_prof[7], 1ull);
-        const unsigned wi = atomicAdd(&g_wave_n, 1u);
-        if (wi < (unsigned)kProfWaves) {
-            g_wave_t[2 * wi] = wt0;
-            g_wave_t[2 * wi + 1] = wall_clock64();
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
-#endif
-    rtd::counters_flush<COUNT>(cnt, counters);
-}
-
-// ------------------------------------------------------------------------ path pool (rt_pool.h)
-// The lane-resident path tracer with the wave's paths in a pool: lanes are traversal slots fed
-// from the wave's traversal queue, ready paths are shaded kPoolBatch at a time by lanes 0..n-1.
-// Parity mode, shards of more than kSpecPixelsPerLane pixels per lane (the 1- and 2-GPU
-// frames).  Exit: every path of the pool retires once the pixel queue is empty (it is then in
-// no ring and no lane), and the loop ends when no lane traverses and both rings are empty.
-// RT_POOL_PARK: the traversal state of the lanes is parked in memory around a shading pass
-// (0: kept in registers, spilled where the compiler decides).
-#ifndef RT_POOL_PARK
-#define RT_POOL_PARK 1
-#endif
-constexpr bool kPoolPark = RT_POOL_PARK != 0;
-// RT_POOL_DEFER_HIT: a finished traversal's hit store waits for the next step's loads (above).
-#ifndef RT_POOL_DEFER_HIT
-#define RT_POOL_DEFER_HIT 1
-#endif
-constexpr bool kPoolDeferHit = RT_POOL_DEFER_HIT != 0;
-// RT_POOL_HITLDS: hits of ready paths in LDS by ready-ring position (below); 0: in the record.
-#ifndef RT_POOL_HITLDS
-#define RT_POOL_HITLDS 1
-#endif
-constexpr bool kPoolHitLds = RT_POOL_HITLDS != 0;
-template <bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMegaWpe, 8)))
-rt_pool_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
-               unsigned long long *queue, const int *order) {
-    const long long n_items = g.n_pixels;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __shared__ float lut[256];
-    __shared__ uint8_t ring_q[4][rtd::kPool], ring_r[4][rtd::kPool];
-    // hits of ready paths by ready-ring position (mod 64): a finished traversal's hit goes to
-    // LDS, not to the path record, so the traversal loop issues no global store (a store would
-    // make the next step's load waits wait for it too: vmcnt counts both)
-    __shared__ float4 hit_slot[4][64];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) lut[k] = sc_in.lut[k];
-    __syncthreads();
-    DevScene sc = sc_in;
-    sc.lut = lut;
-    Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    uint2 spill[rtd::kStack - rtd::kLdsStack];
-    rtd::LdsStackT<rtd::kLdsStack> S{spill};
-    const rtd::GlobalNodes nodes{sc.node};
-    const rtd::NodeRec root = rtd::load_node(sc.node, 0);
-    const rtd::PoolPlanes V{st.mid, st.lanes};
-    const long long wbase = ((long long)blockIdx.x * 4 + wave) * rtd::kPool;   // the wave's first path id
-    uint8_t *rq = ring_q[wave], *rr = ring_r[wave];
-    int qh = 0, qt = 0, rh = 0, rt = 0;   // ring heads / tails (running counts, wave-uniform)
-    bool exhausted = false;
-    for (int q = 0; q < rtd::kPoolPerLane; ++q) {   // every path of the pool takes a pixel
-        const int j = lane + 64 * q;
-        const int pix = rtd::pool_claim(true, queue, n_items, order, exhausted);
-        const int nx = pix >= 0 ? rtd::pool_assign<COUNT>(V, wbase + j, sc, g, pix, root, cnt) : rtd::PN_PIXEL;
-        rtd::pool_push(rq, qt, nx == rtd::PN_QUEUE, j);
-        rtd::pool_push(rr, rt, nx == rtd::PN_READY, j);
-    }
-    rtd::Ray r{};
-    rtd::TravStateU T;   // (defined for every lane: a free lane's state is parked too)
-    T.a = T.b = 0u;
-    T.acc = 1e9f;
-    T.sp = 0;
-    T.phase = rtd::TP_POP;
-    T.best = rtd::Hit{1e9f, 0.f, 0.f, -1};
-    int jc = 0;          // the path this lane traverses (number in the pool)
-    bool trav = false;
-    // A traversal that has ended (done): the path goes to the ready ring at once, its hit to the
-    // path record one step later (pend / ph / pj), by the next step's hook, after that step's
-    // loads have arrived: a store issued before them would make their waits wait for it too
-    // (vmcnt).  Every pending hit is stored before a shading pass reads it (flush).
-    bool pend = false;
-    int pj = 0;
-    rtd::Hit ph{1e9f, 0.f, 0.f, -1};
-    auto flush = [&]() {
-        if (pend) rtd::pool_st(V.C(wbase + pj), make_float4(ph.t, ph.u, ph.v, __int_as_float(ph.prim)));
-        pend = false;
-    };
-    auto finish = [&](bool done) {
-        if constexpr (kPoolHitLds) {
-            // ready-ring entry: path number, bit 7 = the hit is in LDS slot (position % 64); free
-            // unless 64 or more ready paths are ahead of it (then the path record, as below)
-            const unsigned long long m = __ballot(done);
-            if (m) {
-                const int pos = rt + __popcll(m & ((1ull << lane) - 1ull));
-                const bool in_lds = pos - rh < 64;
-                if (done && in_lds)
-                    hit_slot[wave][pos & 63] =
-                        make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
-                if (done && !in_lds)
-                    rtd::pool_st(V.C(wbase + jc), make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim)));
-                if (done) rr[(unsigned)pos % (unsigned)rtd::kPool] = (uint8_t)(jc | (in_lds ? 0x80 : 0));
-                rt += __popcll(m);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-            }
-            return;
-        }
-        if (done) {
-            if constexpr (kPoolDeferHit) {
-                pend = true;
-                pj = jc;
-                ph = T.best;
-            } else {
-                rtd::pool_st(V.C(wbase + jc), make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim)));
-            }
-        }
-        rtd::pool_push(rr, rt, done, jc);
-    };
-    // free lanes take queued paths (ring order)
-    auto refill = [&]() {
-        const unsigned long long fm = __ballot(!trav);
-        const int nq = qt - qh, nf = __popcll(fm);
-        const int take = nf < nq ? nf : nq;
-        if (take <= 0) return;
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-        if (!trav && rank < take) {
-            jc = rq[(unsigned)(qh + rank) % (unsigned)rtd::kPool];
-            r = rtd::pool_load_ray(V, wbase + jc);
-            trav = rtd::trav_start<COUNT>(0u, root.a, root.b, T, cnt);   // (queued rays enter the root box)
-        }
-        qh += take;
-    };
-#ifdef RT_MEGA_PROF
-    // (diagnostics build: the lane-resident kernel's g_mega_prof slots, same meaning)
-    unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
-    __syncthreads();
-    long long tp = clock64();
-    const unsigned long long wt0 = wall_clock64();
-#endif
-    for (;;) {
-        refill();
-        const int nt = __popcll(__ballot(trav)), nready = rt - rh;
-        if (nt == 0 && nready == 0) break;   // (the refill emptied the queue: every path has retired)
-#ifdef RT_MEGA_PROF
-        {
-            const long long t1 = clock64();
-            pf[2] += (unsigned long long)(t1 - tp);
-            tp = t1;
-        }
-#endif
-        if (nt > 0 && nready < rtd::kPoolBatch) {
-            // traversal iterations until kPoolBatch paths are ready or no lane traverses; free
-            // lanes are refilled in batches of kPoolRefill
-            int kt = nt;
-            do {
-#ifdef RT_MEGA_PROF
-                pf[4] += 1;
-                pf[6] += (unsigned long long)kt;
-#endif
-                const bool done = rtd::trav_step_coop<COUNT, kCoopLeavesPlain>(sc, r, T, S, nodes, cnt, trav,
-                                                                               kCoopRoundMinPlain, flush);
-                if (done) trav = false;
-                finish(done);
-                if (__popcll(__ballot(!trav)) >= rtd::kPoolRefill && qt > qh) refill();
-                kt = __popcll(__ballot(trav));
-            } while (kt > 0 && rt - rh < rtd::kPoolBatch);
-            flush();
-#ifdef RT_MEGA_PROF
-            {
-                const long long t1 = clock64();
-                pf[1] += (unsigned long long)(t1 - tp);
-                tp = t1;
-            }
-#endif
-            continue;
-        }
-#ifdef RT_MEGA_PROF
-        pf[3] += 1;
-        pf[5] += (unsigned long long)(nready < 64 ? nready : 64);
-#endif
-        // shading pass: lanes 0..ns-1 shade the oldest ready paths; a lane that traverses
-        // another path keeps its frames, the light walk stacks above them
-        const int ns = nready < 64 ? nready : 64;
-        int nx = rtd::PN_PIXEL;
-        int js = 0;
-        const int sp0 = trav ? T.sp : 0;
-        if constexpr (kPoolPark) {
-            // park the traversal (its ray is the path record's; the rest in the lane's slot of
-            // WfState::st) so that none of it is live across the shading code (every lane
-            // stores and reloads, so no value of a free lane survives the pass either)
-            {
-                const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-                st.st[2 * slot] = make_float4(__uint_as_float(T.a), __uint_as_float(T.b), T.acc,
-                                              __uint_as_float(((uint32_t)T.sp & 255u) | ((uint32_t)T.phase & 255u) << 8 |
-                                                              ((uint32_t)jc & 255u) << 16));
-                st.st[2 * slot + 1] = make_float4(T.best.t, T.best.u, T.best.v, __int_as_float(T.best.prim));
-            }
-        }
-        if (lane < ns) {
-            const int pos = rh + lane;
-            js = rr[(unsigned)pos % (unsigned)rtd::kPool];
-            const bool in_lds = kPoolHitLds && (js & 0x80);
-            js &= 0x7f;
-            const float4 h4 = in_lds ? hit_slot[wave][pos & 63] : rtd::pool_ld(V.C(wbase + js));
-            rtd::OffsetStack<decltype(S)> os{S, sp0};
-            nx = rtd::pool_shade<COUNT>(V, wbase + js, h4, sc, g, st, spp, out, root, os, cnt);
-        }
-        if constexpr (kPoolPark) {
-            {
-                const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-                const float4 a = st.st[2 * slot], b = st.st[2 * slot + 1];
-                const uint32_t w = __float_as_uint(a.w);
-                T.a = __float_as_uint(a.x);
-                T.b = __float_as_uint(a.y);
-                T.acc = a.z;
-                T.sp = (int)(w & 255u);
-                T.phase = (int)((w >> 8) & 255u);
-                jc = (int)((w >> 16) & 255u);
-                T.best = rtd::Hit{b.x, b.y, b.z, __float_as_int(b.w)};
-                r = rtd::pool_load_ray(V, wbase + jc);
-            }
-        }
-        rh += ns;
-        {   // paths whose pixel is done take the next pixel (or retire)
-            const int pix = rtd::pool_claim(lane < ns && nx == rtd::PN_PIXEL, queue, n_items, order, exhausted);
-            if (pix >= 0) nx = rtd::pool_assign<COUNT>(V, wbase + js, sc, g, pix, root, cnt);
-        }
-        rtd::pool_push(rq, qt, lane < ns && nx == rtd::PN_QUEUE, js);
-        rtd::pool_push(rr, rt, lane < ns && nx == rtd::PN_READY, js);
-#ifdef RT_MEGA_PROF
-        {
-            const long long t1 = clock64();
-            pf[0] += (unsigned long long)(t1 - tp);
             tp = t1;
         }
 #endif
@@ -1350,35 +1130,31 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             const long long full_blocks = resident_blocks(d, rt_mega_kernel<false, false, false, true>);
             const bool spec = !fast && !lsplit && !count && !(p->flags & RT_FLAG_NO_RUNAHEAD) &&
                               g.n_pixels * kClaimStride <= kSpecPixelsPerLane * full_blocks * 256;
-            // path pool (rt_pool.h) for the other parity renders; its light walk stacks above a
-            // traversal's frames, so both BVH depths must fit the stack together
-            const bool pool = !fast && !lsplit && !spec && (p->flags & RT_FLAG_POOL) && kClaimStride == 1 &&
-                              s->bvh_depth + s->light_bvh_depth + 6 < (uint32_t)rtd::kStack;
             auto mk = fast ? (count ? rt_mega_kernel<true, true> : rt_mega_kernel<false, true>)
                            : lsplit ? (count ? rt_mega_kernel<true, false, true> : rt_mega_kernel<false, false, true>)
                                     : count ? rt_mega_kernel<true>
                                             : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
-            sched = fast ? RT_SCHED_FAST : lsplit ? RT_SCHED_LIGHT_SPLIT : spec ? RT_SCHED_RUNAHEAD
-                                                                         : pool ? RT_SCHED_POOL : RT_SCHED_LANE;
-            auto pk = count ? rt_pool_kernel<true> : rt_pool_kernel<false>;
-            // pool: kPool paths per wave, so a block serves 256 x kPoolPerLane pixels at once
-            const unsigned blocks = pool ? persistent_blocks(d, pk, (n_items + rtd::kPoolPerLane - 1) / rtd::kPoolPerLane)
-                                         : persistent_blocks(d, mk, n_items * kClaimStride);
-            const long long slots = (long long)blocks * 256 * (pool ? rtd::kPoolPerLane : 1);   // lane slots / paths
-            // records and pool planes are addressed with 32-bit byte offsets (rt_path.h LaneRec)
+            sched = fast ? RT_SCHED_FAST : lsplit ? RT_SCHED_LIGHT_SPLIT : spec ? RT_SCHED_RUNAHEAD : RT_SCHED_LANE;
+            const unsigned blocks = spec && kSpecFill
+                                        ? (unsigned)std::max<long long>(1, std::min<long long>(full_blocks, (n_items + 3) / 4))
+                                        : persistent_blocks(d, mk, n_items * kClaimStride);
+            // the first claim's size per wave (rt_mega_kernel quota), for the spread below
+            const long long first_claim = spec && kSpecFill ? std::min<long long>(64, (n_items + 4LL * blocks - 1) / (4LL * blocks)) : 64;
+            const long long slots = (long long)blocks * 256;   // lane slots
+            // vertex records are addressed with 32-bit byte offsets (rt_path.h LaneRec)
             if ((unsigned long long)slots * (unsigned long long)s->ray_depth * 32ull >= (1ull << 32))
                 return rt_fail(RT_ERR_LIMIT, "rt_render: vertex records beyond 4 GiB");
             int rc = ensure_wf(d, std::max<long long>(g.n_pixels, slots), s->ray_depth);   // vertex records
             if (rc) return rc;
             rtd::WfState w = d->wf;
             w.n = g.n_pixels;
-            w.lanes = slots;   // LaneRec slots (<= the workspace capacity); the pool's record planes
+            w.lanes = slots;   // LaneRec slots (<= the workspace capacity)
             w.round_min = d->ds.n_nodes < kCoopRoundNodes ? kCoopRoundMinSpec : 65;
             int *order = nullptr;
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
                 // the spread deals one pixel of every cost stratum to each claim of 64 of the
-                // launch's first round (one per wave; kPoolPerLane per wave in the pool)
-                rc = launch_order(d, g, stream, 4LL * blocks * (pool ? rtd::kPoolPerLane : 1), 64, &order);
+                // launch's first round (one per wave)
+                rc = launch_order(d, g, stream, 4LL * blocks, first_claim, &order);
                 if (rc) return rc;
                 ordered = true;
             }
@@ -1397,12 +1173,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
             }
 #endif
-            if (pool)
-                hipLaunchKernelGGL(pk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
-                                   (const int *)order);
-            else
-                hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
-                                   (const int *)order, (unsigned *)nullptr, cs);
+            hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
+                               (const int *)order, (unsigned *)nullptr, cs);
             HIP_TRY(hipGetLastError());
             if (fast) {
                 const long long n3 = g.n_pixels * 3;
@@ -1745,7 +1517,20 @@ int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int
         DeviceGuard g(root);
         if (!g.ok) return rt_fail(RT_ERR_DEVICE, "hipSetDevice failed");
         hipStream_t q = rd->fr_stream;
-        for (int d : uniq) HIP_TRY(hipStreamWaitEvent(q, s->dev[d]->fr_last, 0));
+        // The root's own last copy is waited for on its stream.  A peer's copy is waited for on
+        // the host (hipEventSynchronize on the peer's event) before the assembly is queued: a
+        // root-stream wait on an event recorded on another device is the cheaper form, but it
+        // has not run on a multi-GPU box yet, so the host wait stays the
+        // conservative default until it has.
+        for (int d : uniq) {
+            if (d == root) {
+                HIP_TRY(hipStreamWaitEvent(q, s->dev[d]->fr_last, 0));
+            } else {
+                DeviceGuard gp(d);
+                if (!gp.ok) return rt_fail(RT_ERR_DEVICE, "hipSetDevice failed");
+                HIP_TRY(hipEventSynchronize(s->dev[d]->fr_last));
+            }
+        }
         if (H > 0) {
             hipLaunchKernelGGL(rt_rows_scatter_kernel, dim3(4, (unsigned)H), dim3(256), 0, q, (const uint8_t *)stage_u8,
                                frame_u8, row_map, (long long)H, (long long)row_u8);
@@ -1915,7 +1700,7 @@ __global__ void __launch_bounds__(256) coop_check_kernel(const float4 *tri, int 
     const rtd::GlobalNodes gn{nodes};
     bool active = valid;
     for (int it = 0; it < 64 && __any(active); ++it)   // (bounded: 7 triangles, 64 lanes, 8 per round)
-        if (rtd::trav_step_coop<false, kLeaves>(sc, r, T, S, gn, cnt, active, round_min)) active = false;
+        if (rtd::trav_step_coop<false, kLeaves, false>(sc, r, T, S, gn, cnt, active, round_min)) active = false;
     // sequential reference: trav_step's per-lane loop, one triangle at a time
     float acc = 1e9f;
     rtd::Hit best{1e9f, 0.f, 0.f, -1};

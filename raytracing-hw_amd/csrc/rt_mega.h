@@ -495,20 +495,6 @@ constexpr int kSpecWindow = RT_SPEC_WINDOW;   // jobs in flight per pixel at mos
 constexpr bool kSpecLazy = RT_SPEC_LAZY != 0;   // spec_job_end: only frontier ends trigger a pass
 constexpr int kSpecIssue = RT_SPEC_ISSUE;     // runahead jobs a pixel gets per management pass
 static_assert(kSpecWindow >= 1 && kSpecWindow <= 10, "lane table holds 10 slots");
-// Tail window: once at most kSpecTailRecords pixels of a wave are unfinished, each of them may
-// have kSpecWindowTail jobs in flight (and get window - 1 per pass).  A wave's last chains are
-// its critical path and its other lanes are idle by then, while a wide window everywhere
-// costs the full waves lockstep divergence (round 2: windows 6 / 8 at 316 / 326 ms vs 307).
-// 0: one window throughout.
-#ifndef RT_SPEC_TAIL_RECORDS
-#define RT_SPEC_TAIL_RECORDS 0
-#endif
-#ifndef RT_SPEC_WINDOW_TAIL
-#define RT_SPEC_WINDOW_TAIL 6
-#endif
-constexpr int kSpecTailRecords = RT_SPEC_TAIL_RECORDS;
-constexpr int kSpecWindowTail = RT_SPEC_WINDOW_TAIL;
-static_assert(kSpecWindowTail >= kSpecWindow && kSpecWindowTail <= 10, "lane table holds 10 slots");
 // The lanes running jobs f, f+1, ...: 6-bit slots of a 64-bit table (planes 2 and 3 .w).
 __device__ __forceinline__ int spec_tab(unsigned long long t, int q) { return (int)((t >> (6 * q)) & 63ull); }
 __device__ __forceinline__ unsigned long long spec_tab_set(unsigned long long t, int q, int ln) {
@@ -717,12 +703,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         jc.put(lane, done ? lane_sum(L) : V3{0.f, 0.f, 0.f});
         je.put(lane, done ? lane_rng(L) : Rng{0u, 0u, 0.f});
     })
-    // the window of this pass (wave-uniform): the tail window once few records are active
-    unsigned long long act = 0;
-    WAVE_PHASE(lane, { WBALLOT(act, lane, (rm.get(lane) & kRecActive) != 0); })
-    const bool tailw = kSpecTailRecords > 0 && popc64(act) <= kSpecTailRecords;
-    const int win = tailw ? kSpecWindowTail : kSpecWindow;
-    const int issue = tailw ? kSpecWindowTail - 1 : kSpecIssue;
+    constexpr int win = kSpecWindow, issue = kSpecIssue;
     // A. add ended frontier jobs, one per pixel per round, at most `win` rounds
     for (int q = 0; q < win; ++q) {
         WArr<int> prog;

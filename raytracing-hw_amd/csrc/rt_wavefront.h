@@ -580,15 +580,6 @@ struct LdsStackT {
 #ifndef RT_SOA
 #define RT_SOA 0   // 1: SoA node / triangle planes for the coop step (A/B build)
 #endif
-#ifndef RT_TRI_LOAD36
-#define RT_TRI_LOAD36 0   // 1: the coop step loads 36 B of each triangle record, not 48 (A/B)
-#endif
-#ifndef RT_QUAD_NODE_LOAD
-#define RT_QUAD_NODE_LOAD 0   // 1: quad-cooperative pair loads + DPP transpose (A/B)
-#endif
-#ifndef RT_MASK_NODE_LOAD
-#define RT_MASK_NODE_LOAD 0   // 1: the coop step's pair loads under the node lanes' mask (A/B)
-#endif
 
 // One step of the quad reduction: take the partner lane's (t, u, v, index) when its t is
 // less, or equal with a lower index.
@@ -605,36 +596,6 @@ __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, in
     cj = take ? j2 : cj;
 }
 
-#if RT_QUAD_NODE_LOAD
-// One stage of a 4x4 transpose over the lanes of a quad (X[k] at lane L -> X[L] at lane k
-// after both stages): the element at (lane L, register k) whose bit M differs between L and
-// k moves to (L ^ M, k ^ M).
-// Round R of the quad-cooperative pair load: chunk j of the pair of the quad's lane R.
-template <int R, class Nodes>
-__device__ __forceinline__ void quad_load_round(float4 X[4], const Nodes &nodes, uint32_t my, int myn, int j) {
-    constexpr int kCtl = R * 0x55;   // quad_perm [R, R, R, R]
-    const uint32_t ar = (uint32_t)__builtin_amdgcn_mov_dpp((int)my, kCtl, 0xF, 0xF, false);
-    const int nr = __builtin_amdgcn_mov_dpp(myn, kCtl, 0xF, 0xF, false);
-    if (nr) X[R] = nodes.pair(ar)[j];
-}
-template <int CTL, int M>
-__device__ __forceinline__ void quad_transpose_stage(float4 X[4], int lane) {
-    const bool hi = (lane & M) != 0;
-#pragma unroll
-    for (int k0 = 0; k0 < 4; ++k0) {
-        if (k0 & M) continue;
-        const int k1 = k0 | M;
-        float *a = reinterpret_cast<float *>(&X[k0]), *b = reinterpret_cast<float *>(&X[k1]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float send = hi ? a[c] : b[c];
-            const float recv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), CTL, 0xF, 0xF, false));
-            a[c] = hi ? recv : a[c];
-            b[c] = hi ? b[c] : recv;
-        }
-    }
-}
-#endif
 
 // kCoopLeaves: leaf lanes served per round (4 lanes of the wave each); their records take
 // 32 B each per wave in LDS (the caller's kernel budget decides: DESIGN.md §6).
@@ -649,7 +610,14 @@ struct NoHook {
 // before the node test): the pool kernel issues its previous step's hit store there, so that
 // no wait of this step's loads also waits for that store (vmcnt counts loads and stores in
 // issue order).
-template <bool COUNT, int kCoopLeaves, class Stack, class Nodes, class TS, class Hook = NoHook>
+// MASK_LOAD: only the node lanes issue the child-pair loads (the others skip them instead of
+// loading the root's pair).  Round 5 A/B (profiles/r05_memreq_ab.jsonl, two runs): the plain
+// kernel (one GPU, lanes mostly traversing) 1175-1177 vs 1132-1133 ms, the runahead kernel
+// (8-way shards, sparser waves) 202.8-202.9 vs 203.8-204.3 ms mean shard; so the runahead
+// kernel takes it and the plain kernel does not.  Two other request shapes were measured and
+// removed: quad-cooperative pair loads with a DPP transpose (1259 ms, 8-way 233 ms) and 36-B
+// triangle loads (1132-1137 ms, 8-way 204 ms: neutral).
+template <bool COUNT, int kCoopLeaves, bool MASK_LOAD, class Stack, class Nodes, class TS, class Hook = NoHook>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TS &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active, int round_min,
                                                const Hook &hook = Hook{}) {
@@ -669,31 +637,17 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
         q[1] = p1[0];
         q[3] = p1[1];
     }
-#elif RT_QUAD_NODE_LOAD
-    {
-        // Quad-cooperative pair loads: in round r, lane 4g+j loads 16-B chunk j of the pair of
-        // lane 4g+r, so each load instruction touches one 64-B line per quad instead of one
-        // per lane; a 4x4 transpose over the quad (two DPP exchange stages) then gives every
-        // lane the four chunks of its own pair.
-        const int j = lane & 3;
-        const uint32_t my = at_node ? T.a : 0u;
-        const int myn = at_node ? 1 : 0;
-        // (the transpose waits for the loads: it runs after the leaf exchange, as node_step does)
-        quad_load_round<0>(q, nodes, my, myn, j);
-        quad_load_round<1>(q, nodes, my, myn, j);
-        quad_load_round<2>(q, nodes, my, myn, j);
-        quad_load_round<3>(q, nodes, my, myn, j);
-    }
-#elif RT_MASK_NODE_LOAD
-    // (only the node lanes issue the pair loads: the others leave the address unit alone)
-    // (q is read only by node lanes: no initialisation, which would wait on the registers' last loads)
-    if (at_node) {
-        const float4 *p0 = nodes.pair(T.a);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = p0[i];
-    }
 #else
-    {
+    if (MASK_LOAD) {
+        // (only the node lanes issue the pair loads: the others leave the address unit alone;
+        // q is read only by node lanes: no initialisation, which would wait on the registers'
+        // last loads)
+        if (at_node) {
+            const float4 *p0 = nodes.pair(T.a);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = p0[i];
+        }
+    } else {
         const float4 *p0 = nodes.pair(at_node ? T.a : 0u);
 #pragma unroll
         for (int i = 0; i < 4; ++i) q[i] = p0[i];
@@ -729,13 +683,7 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
                 const float4 t0 = t[0], t1 = t[sc.tri_plane], t2 = t[2 * sc.tri_plane];
 #else
                 const float4 *t = sc.tri + 3 * (size_t)k;
-#if RT_TRI_LOAD36
-                // (the test reads 36 of the record's 48 B: the third load is one dword)
-                const float4 t0 = t[0], t1 = t[1];
-                const float2 t2 = make_float2(reinterpret_cast<const float *>(t)[8], 0.f);
-#else
                 const float4 t0 = t[0], t1 = t[1], t2 = t[2];
-#endif
 #endif
                 Ray hr;
                 hr.o = V3{a.x, a.y, a.z};
@@ -772,10 +720,6 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
         }
     }
     hook();
-#if RT_QUAD_NODE_LOAD && !RT_SOA
-    quad_transpose_stage<0xB1, 1>(q, lane);   // lane ^ 1
-    quad_transpose_stage<0x4E, 2>(q, lane);   // lane ^ 2
-#endif
     // node lanes: the pair test
     if (at_node) node_step<COUNT>(q, r, T, stk, cnt);
     if (active && T.phase == TP_POP) return trav_pop(T, stk);

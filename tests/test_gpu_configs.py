@@ -7,7 +7,7 @@ sources, oracle/ref_harness `pixels`, per-pixel RNG convention of SURVEY.md §8c
   C4        sponza proxy 1920x1080x1024, each of the 8 row-block shards of the 8-GPU split
   C5        dragon-100k + sponza proxy 3840x2160x4096, rank 0's shard of the 8-GPU split, and
             64 pixels of each of ranks 1-7 at full spp
-  whole frames: C3 and the headline (and C4 once its golden exists), every row of the float
+  whole frames: C3, the headline and C4, every row of the float
             frame (per-row FNV-1a hashes of the reference's own full render,
             tools/make_goldens.py --frames), 8 full rows, the frame counters, and the sha1 of
             the reference's finished 8-bit frame; rendered on one GPU (the plain kernel) and as

@@ -52,47 +52,23 @@ def test_sums_match_reference(gpu, name, w, h, s, kernel, order):
             st["light_tri_tests"]] == [int(x) for x in c]
 
 
-@pytest.mark.parametrize("count,order", [(True, "heavy"), (True, "natural"), (False, "heavy"), (False, "natural")])
-@pytest.mark.parametrize("name,w,h,s", CASES)
-def test_pool_matches_reference(gpu, name, w, h, s, count, order):
-    """The path-pool schedule (rt_pool.h: a wave's 128 paths in HBM, lanes as traversal slots
-    fed from the wave's queue, ready paths shaded 64 at a time; RT_FLAG_POOL) against the
-    reference's sums, and its traversal counters where counting, in both pixel orders.  These
-    frames have fewer pixels than lanes, so a wave's pool is partly empty from the start and
-    the frame is all tail (runahead off, so the pool takes them)."""
-    scene = gpu.Scene.from_view(rtref.ref_arrays(gpu, name, w, h, s))
-    out, st = _sums(scene, s, count=count, pool=True, runahead=False, natural_order=order == "natural",
-                    heavy_order=order == "heavy")
-    assert st["schedule"] == gpu.SCHED_POOL
-    g = rtref.golden(f"{name}_sums_{w}x{h}x{s}.rtd")
-    ref = g["sums"].reshape(-1, 3)
-    bad = (rtref.bits(out) != rtref.bits(ref)).any(1)
-    assert bad.sum() == 0, f"{bad.sum()} pixels differ, max |d| {np.abs(out - ref).max()}"
-    if count:
-        c = g["counters"]
-        assert [st["rays"], st["aabb_tests"], st["tri_tests"], st["light_queries"], st["light_aabb_tests"],
-                st["light_tri_tests"]] == [int(x) for x in c]
-
-
-def test_pool_many_pixels_per_path_vs_oracle(gpu, oracle):
-    """The pool where every path runs several pixels (a 1920x1080 frame: 2.07 M pixels for at
-    most 655 k paths), 16-sample chains, translucent materials and both orders: the frame
-    equals the lane-resident kernel's, and sampled pixels equal the CPU oracle."""
+def test_many_pixels_per_lane_vs_oracle(gpu, oracle):
+    """The lane-resident kernel where every lane runs several pixels (a 1920x1080 frame: 2.07 M
+    pixels for at most 327 k lane slots), 16-sample chains, translucent materials: both pixel
+    orders give the same frame, and sampled pixels equal the CPU oracle."""
     name, W, H, S = "sponza_mini", 1920, 1080, 16
     a = rtref.ref_arrays(gpu, name, W, H, S)
     a["mesh_f"] = a["mesh_f"].copy()
     a["mesh_f"][::3, 8] = np.float32(0.5)
     scene = gpu.Scene.from_view(a)
     lane, st0 = scene.render_sums(S, runahead=False, heavy_order=True)
-    pool, st1 = scene.render_sums(S, pool=True, runahead=False, heavy_order=True)
-    pool_n, _ = scene.render_sums(S, pool=True, runahead=False, natural_order=True)
-    assert st0["schedule"] == gpu.SCHED_LANE and st1["schedule"] == gpu.SCHED_POOL
-    assert np.array_equal(rtref.bits(lane), rtref.bits(pool))
-    assert np.array_equal(rtref.bits(lane), rtref.bits(pool_n))
+    lane_n, _ = scene.render_sums(S, runahead=False, natural_order=True)
+    assert st0["schedule"] == gpu.SCHED_LANE
+    assert np.array_equal(rtref.bits(lane), rtref.bits(lane_n))
     rng = np.random.default_rng(5)
     for p in rng.choice(W * H, 10, replace=False):
         ref, _, _ = oracle.render(a, S, int(p), int(p) + 1, threads=1)
-        assert np.array_equal(rtref.bits(pool.reshape(-1, 3)[p]), rtref.bits(ref[0])), f"pixel {p}"
+        assert np.array_equal(rtref.bits(lane.reshape(-1, 3)[p]), rtref.bits(ref[0])), f"pixel {p}"
 
 
 @pytest.mark.parametrize("name,w,h,s", CASES)

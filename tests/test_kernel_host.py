@@ -192,25 +192,6 @@ def test_lane_resident_runahead_long_chains(rt, kh, name, w, h, s, waves):
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
 
 
-@pytest.mark.parametrize("tail", [(64, 10), (6, 7)])
-def test_runahead_tail_window(rt, tmp_path_factory, tail):
-    """The tail window (rt_mega.h kSpecTailRecords / kSpecWindowTail: a wave with few
-    unfinished pixels gives each of them more runahead jobs) on long chains, with the window
-    widened for every pass (64 records) and only for a wave's last pixels: the plain per-pixel
-    schedule's bits."""
-    lib = _build_kh(tmp_path_factory, f"-DRT_SPEC_TAIL_RECORDS={tail[0]}", f"-DRT_SPEC_WINDOW_TAIL={tail[1]}")
-    lib.kh_render_mega_spec.argtypes = lib.kh_render_mega.argtypes
-    lib.kh_render_mega_spec.restype = ctypes.c_int
-    for name, w, h, s, waves in [("sponza_mini", 32, 18, 48, 4), ("cornell_blob", 24, 24, 64, 6)]:
-        v, keep = _view(rt, name, w, h, s)
-        want = np.zeros((h * w, 3), np.float32)
-        lib.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
-        out = np.zeros((h * w, 3), np.float32)
-        assert lib.kh_render_mega_spec(ctypes.addressof(v), s, 0, 1, 8, waves, 48, None, out.ctypes.data,
-                                       np.zeros(7, np.uint64).ctypes.data) == 0
-        assert np.array_equal(rtref.bits(out), rtref.bits(want)), name
-
-
 @pytest.mark.parametrize("name,w,h,s,waves", [("cornell_blob", 48, 48, 4, 2), ("sponza_mini", 64, 36, 4, 3)])
 def test_lane_resident_any_pixel_order(rt, kh, name, w, h, s, waves):
     """The ordered render (rt_device.hip launch_order: queue item p renders pixel order[p])

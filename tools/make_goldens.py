@@ -199,6 +199,44 @@ def frame_goldens(meta, save, threads=8):
         print("c5_ranks", meta["configs"]["c5_ranks"], flush=True)
 
 
+C5_ROWS_PER_RANK = 8      # full rows per rank for the C5 row golden (64 rows, 245,760 pixels)
+
+
+def c5_row_goldens(meta, save, threads=6):
+    """C5 (dragon + sponza 3840x2160x4096, the 8-way split) as FULL ROWS: 8 seeded rows of every
+    rank's shard, every pixel of them rendered by the reference at 4096 spp (ref_harness pixels,
+    scene.cpp:31-52).  Kept compact: every row's FNV-1a hash of its float sums, one full row per
+    rank, and per-row totals of the reference's test counters (rays, AABB, triangle, light)."""
+    name, scene, W, H, S, world, _ = CONFIGS[3]
+    out = os.path.join(GOLD, f"{name}_{scene}_rows_{W}x{H}x{S}_w{world}.rtd")
+    if os.path.exists(out) and "c5_rows" in meta.get("configs", {}):
+        return
+    path = scenes.ensure_scene(scene, SCENE_DIR)
+    rows = []
+    for r in range(world):
+        mine = np.array([j for j in range(H) if (j // 8) % world == r])
+        pick = np.sort(np.random.default_rng(3000 + r).choice(mine, C5_ROWS_PER_RANK, replace=False))
+        rows.extend(int(j) for j in pick)
+    rows = np.array(rows, np.int64)
+    idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.int64)
+    lst = f"/tmp/{name}_rows_idx.i64"
+    idx.tofile(lst)
+    raw = f"/tmp/{name}_{scene}_rows_{W}x{H}x{S}_full.rtd"
+    info = harness("pixels", path, W, H, S, lst, raw, threads)
+    d = rtdump.load(raw)
+    assert np.array_equal(d["index"], idx)
+    sums = d["sums"].reshape(len(rows), W, 3).astype(np.float32)
+    pc = d["pixel_counters"].reshape(len(rows), W, 6).astype(np.uint64).sum(axis=1)
+    full = np.arange(0, len(rows), C5_ROWS_PER_RANK)          # the first picked row of each rank
+    rtdump.save(out, {"rows": rows.astype(np.int32), "row_fnv1a": row_hash(sums), "full_rows": rows[full].astype(np.int32),
+                      "full_row_sums": sums[full], "row_counters": pc})
+    meta.setdefault("configs", {})["c5_rows"] = {
+        "scene": scene, "width": W, "height": H, "spp": S, "world": world, "rows_per_rank": C5_ROWS_PER_RANK,
+        "file": os.path.basename(out), "pixels": info}
+    print("c5_rows", meta["configs"]["c5_rows"], flush=True)
+    save(meta)
+
+
 SHIPPED = [("cornell", 128, 128, 256), ("sponza_mini", 128, 72, 256)]
 
 
@@ -222,13 +260,16 @@ def main():
         with open(path, "w") as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return
-    if "--frames" in sys.argv:
+    if "--frames" in sys.argv or "--c5rows" in sys.argv:
         path = os.path.join(GOLD, "golden_meta.json")
         meta = json.load(open(path))
         def save(m):
             with open(path, "w") as f:
                 json.dump(m, f, indent=1, sort_keys=True)
-        frame_goldens(meta, save)
+        if "--c5rows" in sys.argv:
+            c5_row_goldens(meta, save)
+        else:
+            frame_goldens(meta, save)
         save(meta)
         return
     if "--configs" in sys.argv:

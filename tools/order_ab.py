@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--natural", type=int, default=1)
+    ap.add_argument("--shard-steps", type=int, default=1)
     args = ap.parse_args()
     rt = bench.import_pkg()
     path = bench.load_scenes_module().ensure_scene(args.scene, os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes"))
@@ -36,6 +37,9 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     res = {"lib": os.environ.get("RT_LIB", "default")}
 
+    import hashlib
+    shard_hash = hashlib.sha1()
+
     def t(world, rank, steps, natural):
         out = torch.zeros(rtdist.max_shard_rows(H, world) * W * 3, dtype=torch.float32, device="cuda")
         ms, order = [], []
@@ -44,15 +48,22 @@ def main():
                                      natural_order=natural)
             ms.append(st["render_ms"])
             order.append(st["order_ms"])
+        if world > 1 and not natural:
+            shard_hash.update(out.cpu().numpy().tobytes())
         return min(ms), min(order)
 
     t(1, 0, 1, False)   # warm
     res["full_ms"], res["full_order_ms"] = t(1, 0, args.steps, False)
+    full = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+    scene.render_device(full.data_ptr(), stream, spp=S, rank=0, world=1)
+    torch.cuda.synchronize()
+    res["full_sha1"] = __import__("hashlib").sha1(full.cpu().numpy().tobytes()).hexdigest()[:16]
     if args.natural:
         res["full_natural_ms"], _ = t(1, 0, args.steps, True)
-    sh = [t(args.world, r, 1, False)[0] for r in range(args.world)]
+    sh = [t(args.world, r, args.shard_steps, False)[0] for r in range(args.world)]
     res[f"shard{args.world}_ms"] = [round(x, 1) for x in sh]
     res[f"shard{args.world}_max_ms"] = max(sh)
+    res[f"shard{args.world}_sha1"] = shard_hash.hexdigest()[:16]   # the shards' float sums (same bits across builds)
     if args.natural:
         shn = [t(args.world, r, 1, True)[0] for r in range(args.world)]
         res[f"shard{args.world}_natural_max_ms"] = max(shn)

@@ -3,7 +3,7 @@
 
     python tools/pmc_compare.py DIR_OR_PREFIX [kernel-substring ...]
 
-For every kernel whose name contains one of the substrings (default: rt_mega_kernel, rt_pool_kernel):
+For every kernel whose name contains one of the substrings (default: rt_mega_kernel):
 duration, VALU / SALU instructions, lane utilisation (SQ_THREAD_CYCLES_VALU / (ACTIVE_INST_VALU x 64)),
 wait share, VALU instructions per SIMD-cycle, HBM-side bytes (2 x FETCH_SIZE + WRITE_SIZE)."""
 import csv
@@ -29,7 +29,7 @@ def load(d):
 
 def main():
     d = sys.argv[1]
-    keys = sys.argv[2:] or ["rt_mega_kernel", "rt_pool_kernel"]
+    keys = sys.argv[2:] or ["rt_mega_kernel"]
     for k, v in load(d).items():
         if not any(s in k for s in keys):
             continue
