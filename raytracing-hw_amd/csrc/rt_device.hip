@@ -303,6 +303,29 @@ __device__ unsigned long long g_mega_seg[8];   // shading segments (rt_path.h RT
 constexpr int kProfWaves = 16384;
 __device__ unsigned long long g_wave_t[2 * kProfWaves];
 __device__ unsigned int g_wave_n;
+// time buckets of 5 ms (wall clock since the wave's start; the waves of a launch start within
+// microseconds of each other): [0] traversal iterations [1] traversing lanes summed over them
+// [2] lanes holding work (state != idle) summed over them [3] shading passes [4] READY lanes
+// summed over them [5] management passes (runahead kernel)
+constexpr int kTb = 256, kTbN = 6;
+constexpr unsigned long long kTbTicks = 500000;   // 5 ms at 100 MHz
+__device__ unsigned long long g_tb[kTb * kTbN];
+struct TbAcc {
+    int b = 0;
+    unsigned long long c[kTbN] = {0, 0, 0, 0, 0, 0};
+    __device__ void at(unsigned long long t0) {   // (every lane; lane 0 flushes)
+        const unsigned long long e = (wall_clock64() - t0) / kTbTicks;
+        const int nb = e < (unsigned long long)kTb ? (int)e : kTb - 1;
+        if (nb != b) flush(nb);
+    }
+    __device__ void flush(int nb) {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < kTbN; ++k)
+                if (c[k]) atomicAdd(&g_tb[b * kTbN + k], c[k]);
+        for (int k = 0; k < kTbN; ++k) c[k] = 0;
+        b = nb;
+    }
+};
 #endif
 // FAST (RT_FLAG_FAST): queue items are (chunk, pixel) work units of `cs`
 // samples with per-sample Philox seeds; `out` is then the chunk-major partial buffer that
@@ -353,9 +376,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
+    if (threadIdx.x < 8) rtd::spec_prof_lds[threadIdx.x] = 0;
     __syncthreads();
     long long tp = clock64();
     const unsigned long long wt0 = wall_clock64();
+    TbAcc tbk;
 #endif
     for (;;) {
         if (!exhausted) {   // lanes without work take the next items (one atomic per wave)
@@ -393,6 +418,9 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #ifdef RT_MEGA_PROF
                     const long long c0 = clock64();
 #endif
+#ifdef RT_MEGA_PROF
+                    tbk.c[5] += 1;
+#endif
                     wave_room = rtd::spec_manage(rtd::SpecLanes{L}, sc, g,
                                                  rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, spp,
                                                  out, root);
@@ -429,6 +457,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             tp = t1;
             pf[shade_now ? 3 : 4] += 1;
             pf[shade_now ? 5 : 6] += (unsigned long long)(shade_now ? nr : nt);
+            tbk.at(wt0);
+            if (shade_now) {
+                tbk.c[3] += 1;
+                tbk.c[4] += (unsigned long long)nr;
+            }
         }
 #endif
         if (kInnerTrav && !LSPLIT && !shade_now) {
@@ -452,6 +485,9 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #ifdef RT_MEGA_PROF
                 pf[4] += 1;
                 pf[6] += (unsigned long long)kt;
+                tbk.c[0] += 1;
+                tbk.c[1] += (unsigned long long)kt;
+                tbk.c[2] += (unsigned long long)__popcll(__ballot(L.state != rtd::M_IDLE));
 #endif
             } while (true);
         } else {
@@ -467,6 +503,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #endif
     }
 #ifdef RT_MEGA_PROF
+    tbk.flush(tbk.b);
     if (lane == 0) {
         for (int k = 0; k < 7; ++k) atomicAdd(&g_mega_prof[k], pf[k]);
         atomicAdd(&g_mega_prof[7], 1ull);
@@ -478,6 +515,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     }
     __syncthreads();
     if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
+    if (threadIdx.x < 8) atomicAdd(&rtd::g_spec_prof[threadIdx.x], rtd::spec_prof_lds[threadIdx.x]);
 #endif
     rtd::counters_flush<COUNT>(cnt, counters);
 }
@@ -1171,6 +1209,8 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(rtd::g_spec_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
+                static const std::vector<unsigned long long> ztb(kTb * kTbN, 0ull);
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tb), ztb.data(), ztb.size() * 8, 0, hipMemcpyHostToDevice, stream));
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
@@ -1219,6 +1259,27 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                         std::fprintf(stderr, "[mega prof] wave end ms: p10=%.1f p25=%.1f p50=%.1f p75=%.1f p90=%.1f p99=%.1f max=%.1f\n",
                                      ends[nw / 10], ends[nw / 4], ends[nw / 2], ends[3 * nw / 4], ends[9 * nw / 10],
                                      ends[99 * (size_t)nw / 100], ends[nw - 1]);
+                        // per 5-ms bucket: waves alive, traversal iterations per alive wave, lanes per
+                        // iteration (traversing, holding work), shading passes, READY lanes per pass,
+                        // management passes
+                        std::vector<unsigned long long> tbv(kTb * kTbN);
+                        HIP_TRY(hipMemcpyFromSymbolAsync(tbv.data(), HIP_SYMBOL(g_tb), tbv.size() * 8, 0, hipMemcpyDeviceToHost, stream));
+                        HIP_TRY(hipStreamSynchronize(stream));
+                        const int nbk = std::min(kTb, (int)(ends[nw - 1] / 5.0) + 1);
+                        for (int b = 0; b < nbk; ++b) {
+                            double alive = 0;   // wave-buckets alive (fraction of the bucket)
+                            for (unsigned i = 0; i < nw; ++i) {
+                                const double s0 = (double)(wt[2 * i] - t0) / 1e5, e0 = (double)(wt[2 * i + 1] - t0) / 1e5;
+                                const double lo = std::max(s0, 5.0 * b), hi = std::min(e0, 5.0 * (b + 1));
+                                if (hi > lo) alive += (hi - lo) / 5.0;
+                            }
+                            const unsigned long long *c = &tbv[(size_t)b * kTbN];
+                            std::fprintf(stderr, "[mega tb] t=%3d-%3d ms waves=%.0f iters/wave=%.0f trav_lanes=%.1f busy_lanes=%.1f "
+                                         "shades/wave=%.1f ready/shade=%.1f passes/wave=%.1f\n", 5 * b, 5 * b + 5, alive,
+                                         alive > 0 ? c[0] / alive : 0.0, c[0] ? (double)c[1] / c[0] : 0.0,
+                                         c[0] ? (double)c[2] / c[0] : 0.0, alive > 0 ? c[3] / alive : 0.0,
+                                         c[3] ? (double)c[4] / c[3] : 0.0, alive > 0 ? c[5] / alive : 0.0);
+                        }
                     }
                 }
                 unsigned long long sp[8];

@@ -17,6 +17,9 @@
 // to memory (LaneRec, indexed by lane slot).  Same per-pixel arithmetic, so bit-identical output.
 #pragma once
 #include "rt_wavefront.h"
+#if !defined(__HIPCC__)
+#include <algorithm>   // (host emulation of wave_order)
+#endif
 
 namespace rtd {
 
@@ -459,8 +462,11 @@ __device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevSce
 // [0] management passes [1] their cycles (per wave) [2] frontier jobs issued [3] runahead jobs
 // issued [4] jobs added [5] of them runahead jobs [6] invalidations [7] waves that reached a tail
 #if defined(RT_MEGA_PROF) && defined(__HIPCC__)
+// (per-block LDS sums, added to g_spec_prof once at the end of the kernel: global atomics on
+// eight words from every wave serialised the runahead kernel)
 __device__ unsigned long long g_spec_prof[8];
-#define RT_SPEC_STAT(k, v) atomicAdd(&::rtd::g_spec_prof[k], (unsigned long long)(v))
+__shared__ unsigned long long spec_prof_lds[8];
+#define RT_SPEC_STAT(k, v) atomicAdd(&::rtd::spec_prof_lds[k], (unsigned long long)(v))
 #elif !defined(__HIPCC__)
 inline unsigned long long g_spec_prof[8];   // host test harness
 #define RT_SPEC_STAT(k, v) (::rtd::g_spec_prof[k] += (unsigned long long)(v))
@@ -574,6 +580,52 @@ struct SpecLanes {
     MegaLane *W;
     MegaLane &operator[](int l) const { return W[l]; }
 };
+#endif
+
+// Runahead priority (RT_SPEC_PRIO): the order in which records with room in their window get
+// the wave's idle lanes.  0: record (lane) order, which at the tail's start is the pre-pass's
+// heaviest-first order.  1: fewest samples added first (ties by lane): every chain of an 8-way
+// shard starts at the same time, so the chain with the smallest frontier is the one furthest
+// behind (remaining time ~ elapsed x (spp - f) / f), and it is the one that ends the wave.
+#ifndef RT_SPEC_PRIO
+#define RT_SPEC_PRIO 0
+#endif
+constexpr bool kSpecPrio = RT_SPEC_PRIO != 0;
+// RT_SPEC_LATE=K (A/B): runahead jobs only once at most K records of the wave are unfinished
+// (0: from the tail's start).  Frontier jobs are issued either way.
+#ifndef RT_SPEC_LATE
+#define RT_SPEC_LATE 0
+#endif
+constexpr int kSpecLate = RT_SPEC_LATE;
+
+// srec[k] = the record at position k of the ascending order of key (keys distinct: the lane
+// is in their low 6 bits), rank[r] = the position of record r.  GPU: a bitonic sort over the
+// wave's lanes (21 exchange steps), then the inverse permutation by ds_permute.
+#if defined(__HIPCC__)
+__device__ __forceinline__ void wave_order(const WArr<uint32_t> &key, WArr<int> &srec, WArr<int> &rank) {
+    const int lane = (int)(threadIdx.x & 63);
+    uint32_t k = key.v;
+#pragma unroll
+    for (int b = 2; b <= 64; b <<= 1)
+#pragma unroll
+        for (int j = b >> 1; j > 0; j >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)k, j, 64);
+            const bool keep_min = ((lane & j) == 0) == ((lane & b) == 0);
+            k = keep_min ? (o < k ? o : k) : (o > k ? o : k);
+        }
+    srec.v = (int)(k & 63u);
+    rank.v = __builtin_amdgcn_ds_permute(srec.v << 2, lane);   // lane srec[k] receives k
+}
+#else
+inline void wave_order(const WArr<uint32_t> &key, WArr<int> &srec, WArr<int> &rank) {
+    uint32_t k[64];
+    for (int l = 0; l < 64; ++l) k[l] = key.get(l);
+    std::sort(k, k + 64);
+    for (int p = 0; p < 64; ++p) {
+        srec.put(p, (int)(k[p] & 63u));
+        rank.put((int)(k[p] & 63u), p);
+    }
+}
 #endif
 
 // Position of the i-th (from 0) set bit of m (m has more than i set bits).
@@ -803,10 +855,16 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
     // C2. runahead: idle lanes take the next jobs of pixels with room in their window
     WArr<int> room, incl;
     unsigned long long idle2 = 0;
+    bool late_ok = true;
+    if constexpr (kSpecLate > 0) {
+        unsigned long long act = 0;
+        WAVE_PHASE(lane, { WBALLOT(act, lane, (rm.get(lane) & kRecActive) != 0); })
+        late_ok = popc64(act) <= kSpecLate;
+    }
     WAVE_PHASE(lane, {
         int rr = 0;
         const uint32_t m = rm.get(lane);
-        if ((m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane)) {
+        if (late_ok && (m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane)) {
             const int w = win - (int)(rn.get(lane) - rf.get(lane)), left = spp - (int)rn.get(lane);
             rr = w < left ? w : left;
             rr = rr < 0 ? 0 : (rr < issue ? rr : issue);
@@ -814,9 +872,26 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         room.put(lane, rr);
         WBALLOT(idle2, lane, lanes[lane].state == M_IDLE);
     })
+    // the order in which records take idle lanes (RT_SPEC_PRIO): position k holds record
+    // srec[k]; sroom / incl: room and its inclusive prefix sum in that order
+    WArr<int> srec, rank, sroom;
+    if constexpr (kSpecPrio) {
+        WArr<uint32_t> key;
+        WAVE_PHASE(lane, {
+            key.put(lane, room.get(lane) > 0 ? (rf.get(lane) << 6 | (uint32_t)lane) : (0xffffffc0u | (uint32_t)lane));
+        })
+        wave_order(key, srec, rank);
+        WAVE_PHASE(lane, { sroom.put(lane, room.at(srec.get(lane))); })
+    } else {
+        WAVE_PHASE(lane, {
+            srec.put(lane, lane);
+            rank.put(lane, lane);
+            sroom.put(lane, room.get(lane));
+        })
+    }
 #if defined(__HIPCC__)
     {
-        int x = room.v;
+        int x = sroom.v;
         const int lane = (int)(threadIdx.x & 63);
         for (int d = 1; d < 64; d <<= 1) {
             const int y = __shfl_up(x, (unsigned)d, 64);
@@ -825,16 +900,16 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         incl.v = x;
     }
 #else
-    for (int l = 0, t = 0; l < 64; ++l) incl.put(l, t += room.get(l));
+    for (int l = 0, t = 0; l < 64; ++l) incl.put(l, t += sroom.get(l));
 #endif
     const int total = incl.at(63), n_idle2 = popc64(idle2);
     WAVE_PHASE(lane, {
         MegaLane &L = lanes[lane];
         const int i = ((idle2 >> lane) & 1ull) ? popc64(idle2 & ((1ull << lane) - 1ull)) : (1 << 30);
-        int r = 0;   // first record with incl > i
+        int k = 0;   // first position with incl > i
         for (int w = 32; w > 0; w >>= 1)
-            if (incl.at(r + w - 1) <= i) r += w;
-        const int incl_r = incl.at(r), room_r = room.at(r);
+            if (incl.at(k + w - 1) <= i) k += w;
+        const int incl_r = incl.at(k), room_r = sroom.at(k), r = srec.at(k);
         const uint32_t pix = rp.at(r), n = rn.at(r), e = re.at(r);
         Rng Y = ry.at(r);
         if (i < total) {
@@ -847,7 +922,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         }
     })
     WAVE_PHASE(lane, {   // record side: its takers are idle lanes excl .. excl + taken - 1
-        const int rr = room.get(lane), excl = incl.get(lane) - rr;
+        const int rr = room.get(lane), excl = incl.at(rank.get(lane)) - rr;
         int taken = n_idle2 - excl < rr ? n_idle2 - excl : rr;
         taken = taken < 0 ? 0 : taken;
         const int last = taken > 0 ? nth_bit(idle2, excl + taken - 1) : lane;
@@ -875,7 +950,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         const uint32_t m = rm.get(lane);
         const uint32_t f = rf.get(lane), n = rn.get(lane);
         const bool rm_room = (m & kRecActive) &&
-                             (n == f || ((m & kRecXf) && (int)(n - f) < win && (int)n < spp));
+                             (n == f || (late_ok && (m & kRecXf) && (int)(n - f) < win && (int)n < spp));
         WBALLOT(roomy, lane, rm_room);
     })
     return roomy != 0;

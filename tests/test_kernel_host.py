@@ -192,6 +192,25 @@ def test_lane_resident_runahead_long_chains(rt, kh, name, w, h, s, waves):
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
 
 
+@pytest.mark.parametrize("prio", [0, 1])
+def test_runahead_priority_orders(rt, tmp_path_factory, prio):
+    """The order in which records take idle lanes (rt_mega.h RT_SPEC_PRIO: record order, or
+    fewest samples added first through the wave sort wave_order) over long chains and a short
+    frame with more lanes than pixels: the plain per-pixel schedule's bits either way."""
+    lib = _build_kh(tmp_path_factory, f"-DRT_SPEC_PRIO={prio}")
+    lib.kh_render_mega_spec.argtypes = lib.kh_render_mega.argtypes
+    lib.kh_render_mega_spec.restype = ctypes.c_int
+    for name, w, h, s, waves in [("sponza_mini", 32, 18, 48, 4), ("cornell_blob", 24, 24, 64, 6),
+                                 ("practice6_1", 40, 30, 12, 40)]:
+        v, keep = _view(rt, name, w, h, s)
+        want = np.zeros((h * w, 3), np.float32)
+        lib.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
+        out = np.zeros((h * w, 3), np.float32)
+        assert lib.kh_render_mega_spec(ctypes.addressof(v), s, 0, 1, 8, waves, 48, None, out.ctypes.data,
+                                       np.zeros(7, np.uint64).ctypes.data) == 0
+        assert np.array_equal(rtref.bits(out), rtref.bits(want)), name
+
+
 @pytest.mark.parametrize("name,w,h,s,waves", [("cornell_blob", 48, 48, 4, 2), ("sponza_mini", 64, 36, 4, 3)])
 def test_lane_resident_any_pixel_order(rt, kh, name, w, h, s, waves):
     """The ordered render (rt_device.hip launch_order: queue item p renders pixel order[p])
