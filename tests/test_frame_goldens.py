@@ -41,3 +41,22 @@ def test_bench_knows_the_reference_frame():
     assert b.reference_frame_sha1("sponza", 1920, 1080, 256) == f["frame_u8_sha1"]
     assert b.reference_frame_sha1("sponza", 1920, 1080, 1024) == FRAMES["c4"]["frame_u8_sha1"]
     assert b.reference_frame_sha1("sponza", 1920, 1080, 64) is None
+
+
+def test_c5_row_golden_is_consistent():
+    """The C5 full-row golden (tools/make_goldens.py --c5rows): 8 rows of each rank's shard of
+    the 8-way split (rows with (row / 8) % 8 == rank), the full rows' hashes equal their
+    entries, and the per-row counters add up to the reference's totals for those pixels."""
+    c = json.load(open(os.path.join(rtref.GOLD, "golden_meta.json")))["configs"]["c5_rows"]
+    g = rtref.golden(c["file"])
+    rows = g["rows"].astype(np.int64)
+    per = c["rows_per_rank"]
+    assert len(rows) == c["world"] * per == len(np.unique(rows))
+    for rank in range(c["world"]):
+        assert all((int(r) // 8) % c["world"] == rank for r in rows[rank * per:(rank + 1) * per])
+    assert np.array_equal(g["full_rows"], rows[::per])
+    assert np.array_equal(rtref.row_hash(g["full_row_sums"]), g["row_fnv1a"][::per])
+    tot = g["row_counters"].sum(axis=0)
+    p = c["pixels"]
+    assert [int(x) for x in tot] == [p["rays"], p["aabb"], p["tri"], p["light_queries"], p["light_aabb"], p["light_tri"]]
+    assert p["pixels"] == len(rows) * c["width"]

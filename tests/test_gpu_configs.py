@@ -5,8 +5,9 @@ sources, oracle/ref_harness `pixels`, per-pixel RNG convention of SURVEY.md §8c
   C3        sponza proxy 1024x1024x256, whole frame on one GPU
   headline  sponza proxy 1920x1080x256, whole frame on one GPU
   C4        sponza proxy 1920x1080x1024, each of the 8 row-block shards of the 8-GPU split
-  C5        dragon-100k + sponza proxy 3840x2160x4096, rank 0's shard of the 8-GPU split, and
-            64 pixels of each of ranks 1-7 at full spp
+  C5        dragon-100k + sponza proxy 3840x2160x4096, every rank's shard of the 8-GPU split:
+            64 FULL rows (8 per rank) against the reference's render of them, 256 seeded pixels
+            of rank 0 and 64 of each of ranks 1-7
   whole frames: C3, the headline and C4, every row of the float
             frame (per-row FNV-1a hashes of the reference's own full render,
             tools/make_goldens.py --frames), 8 full rows, the frame counters, and the sha1 of
@@ -95,11 +96,26 @@ def test_c4_every_shard_matches_reference(gpu):
     assert checked == len(g["index"])
 
 
-def test_c5_shard_matches_reference(gpu):
+_c5 = {}
+
+
+def _c5_shard(gpu, rank):
+    """Rank `rank`'s shard of C5's 8-way split at 4096 spp (rendered once per module: three
+    tests read it)."""
     c = META["c5"]
     W, H, S, world = c["width"], c["height"], c["spp"], c["world"]
-    scene = _scene(gpu, c["scene"], W, H, S)
-    out, st = scene.render_sums(S, rank=0, world=world)
+    if rank not in _c5:
+        scene = _scene(gpu, c["scene"], W, H, S)
+        out, st = scene.render_sums(S, rank=rank, world=world)
+        assert st["samples"] == out.shape[0] * W * S
+        _c5[rank] = out
+    return _c5[rank]
+
+
+def test_c5_shard_matches_reference(gpu):
+    c = META["c5"]
+    W, H, world = c["width"], c["height"], c["world"]
+    out = _c5_shard(gpu, 0)
     g = rtref.golden(c["file"])
     assert _check(out, gpu.shard_rows(H, 0, world), W, g, world, 0) == len(g["index"])
 
@@ -126,14 +142,37 @@ def test_c5_fast_mode_full_spp(gpu, oracle):
 def test_c5_ranks_1_to_7_match_reference(gpu):
     """64 seeded pixels of each of ranks 1-7 of C5's 8-way split at 4096 spp (rank 0 above)."""
     c = META["c5_ranks"]
-    W, H, S, world = c["width"], c["height"], c["spp"], c["world"]
-    scene = _scene(gpu, c["scene"], W, H, S)
+    W, H, world = c["width"], c["height"], c["world"]
     g = rtref.golden(c["file"])
     checked = 0
     for rank in c["ranks"]:
-        out, _ = scene.render_sums(S, rank=rank, world=world)
-        checked += _check(out, gpu.shard_rows(H, rank, world), W, g, world, rank)
+        checked += _check(_c5_shard(gpu, rank), gpu.shard_rows(H, rank, world), W, g, world, rank)
     assert checked == len(g["index"]) == 64 * len(c["ranks"])
+
+
+def test_c5_full_rows_every_rank_match_reference(gpu):
+    """64 FULL rows of C5 (dragon + sponza 3840x2160 at 4096 spp), 8 seeded rows of every
+    rank's shard of the 8-way split, rendered by the reference here (tools/make_goldens.py
+    --c5rows: 245,760 pixels, 3,911 s on 6 threads; scene.cpp:31-52): every row's FNV-1a hash
+    of its float sums, and one row per rank bit for bit."""
+    c = META["c5_rows"]
+    W, H, world = c["width"], c["height"], c["world"]
+    g = rtref.golden(c["file"])
+    rows = g["rows"].astype(np.int64)
+    assert len(rows) == world * c["rows_per_rank"]
+    got = np.zeros((len(rows), W, 3), np.float32)
+    for rank in range(world):
+        mine = gpu.shard_rows(H, rank, world)
+        pos = {int(r): k for k, r in enumerate(mine)}
+        out = _c5_shard(gpu, rank)
+        for i, r in enumerate(rows):
+            if int(r) in pos:
+                got[i] = out[pos[int(r)]]
+    bad = np.nonzero(rtref.row_hash(got) != g["row_fnv1a"])[0]
+    assert len(bad) == 0, f"{len(bad)} of {len(rows)} rows differ, first rows {rows[bad[:8]]}"
+    for r, want in zip(g["full_rows"], g["full_row_sums"]):
+        i = int(np.nonzero(rows == r)[0][0])
+        assert np.array_equal(rtref.bits(got[i]), rtref.bits(want)), f"row {r}"
 
 
 @pytest.mark.parametrize("world", [4, 8])
