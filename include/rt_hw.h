@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6   /* 6: RT_FLAG_POOL and RT_SCHED_POOL removed (the path pool, round 5) */
 
 enum rt_status {
     RT_OK = 0,

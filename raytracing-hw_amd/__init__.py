@@ -44,7 +44,7 @@ class RtSceneView(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 5          # include/rt_hw.h RT_ABI_VERSION
+ABI_VERSION = 6          # include/rt_hw.h RT_ABI_VERSION
 KERNEL_LANE = 0          # RT_KERNEL_LANE: lane-resident persistent kernel (default)
 KERNEL_WAVEFRONT = 4     # RT_KERNEL_WAVEFRONT: init / extend / shade launches
 FLAG_KERNEL_TIMES = 1    # RT_FLAG_KERNEL_TIMES

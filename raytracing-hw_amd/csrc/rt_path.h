@@ -663,15 +663,36 @@ __device__ __forceinline__ V3 scene_sample(const DevScene &sc, V3 pos, V3 N, V3 
 // caller must compare states, not assume them (rt_mega.h spec_manage does).  Used by the
 // speculative sample runahead: a pixel's sample t+1 starts from the state sample t ends in,
 // and for a path of ray_depth vertices that state is rng_skip_sample(start of t, ray_depth).
+// The polar normals' values are not needed to advance the state, except the cached one: the
+// state's `saved` is x * mult of the last pair drawn (rng_normal), so only that pair's logf and
+// sqrtf are evaluated, once, at the end (same operations, same bits).
+__device__ __forceinline__ void rng_normal_skip(Rng &r, bool &gen, float &lx, float &lr2) {
+    if (r.saved_avail) {
+        r.saved_avail = 0;
+        return;
+    }
+    float x, y, r2;
+    do {
+        x = 2.0f * rng_canonical(r) - 1.0f;
+        y = 2.0f * rng_canonical(r) - 1.0f;
+        r2 = x * x + y * y;
+    } while (r2 > 1.0f || r2 == 0.0f);
+    gen = true;
+    lx = x;
+    lr2 = r2;
+    r.saved_avail = 1;
+}
 __device__ __forceinline__ void rng_skip_sample(Rng &r, int k, int n_lights) {
     (void)rng_next(r);   // rng_offset x 2: one engine draw each
     (void)rng_next(r);
+    bool gen = false;
+    float lx = 0.f, lr2 = 1.f;
     for (int v = 0; v < k; ++v) {
         const int b = mixture_pick(r, n_lights);
         if (b == 0) {
-            (void)rng_normal(r);
-            (void)rng_normal(r);
-            (void)rng_normal(r);
+            rng_normal_skip(r, gen, lx, lr2);
+            rng_normal_skip(r, gen, lx, lr2);
+            rng_normal_skip(r, gen, lx, lr2);
         } else if (b == 1) {
             float ux, uy;
             disc_draw(r, ux, uy);
@@ -680,6 +701,10 @@ __device__ __forceinline__ void rng_skip_sample(Rng &r, int k, int n_lights) {
             (void)rng_next(r);
             (void)rng_next(r);
         }
+    }
+    if (gen) {
+        const float mult = sqrtf(-2.0f * rtm::logf_glibc(lr2) / lr2);
+        r.saved = lx * mult;
     }
 }
 

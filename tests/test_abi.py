@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 5
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 6
     assert ctypes.sizeof(rt.RtParams) == 36
     assert ctypes.sizeof(rt.RtStats) == 9 * 8 + 3 * 8 + 3 * 8 + 3 * 8 + 8   # ABI 5: + schedule
 
