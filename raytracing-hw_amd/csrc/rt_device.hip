@@ -348,6 +348,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     // linear decode is computed: rt_path.h texel_decode)
     __shared__ float lut[256];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) lut[k] = sc_in.lut[k];
+    if constexpr (kSpec && rtd::kSpecShare) {   // the block's offer board (rt_mega.h RT_SPEC_SHARE)
+        for (int k = threadIdx.x; k < rtd::kOffers * rtd::kOfWords; k += blockDim.x) rtd::spec_board()[k] = 0u;
+        if (threadIdx.x == 0) rtd::spec_block_active()[0] = 0;
+        if (threadIdx.x < 4) rtd::spec_fdone()[threadIdx.x] = 0;
+    }
     __syncthreads();
     DevScene sc = sc_in;
     sc.lut = lut;
@@ -376,7 +381,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
-    if (threadIdx.x < 8) rtd::spec_prof_lds[threadIdx.x] = 0;
+    if (threadIdx.x < 16) rtd::spec_prof_lds[threadIdx.x] = 0;
     __syncthreads();
     long long tp = clock64();
     const unsigned long long wt0 = wall_clock64();
@@ -414,7 +419,10 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             }
             if (tail) {
                 wave_room |= rtd::spec_hint_take();
-                if (__any(L.state == rtd::M_DONE_NEW) || (wave_room && __any(L.state == rtd::M_IDLE))) {
+                bool share_pass = false;   // RT_SPEC_SHARE: an offer of ours is done, or one to take
+                if constexpr (rtd::kSpecShare)
+                    share_pass = rtd::spec_fdone_take() || (__any(L.state == rtd::M_IDLE) && rtd::spec_foreign_open());
+                if (__any(L.state == rtd::M_DONE_NEW) || share_pass || (wave_room && __any(L.state == rtd::M_IDLE))) {
 #ifdef RT_MEGA_PROF
                     const long long c0 = clock64();
 #endif
@@ -431,7 +439,13 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                     }
 #endif
                 }
-                if (!__any(L.state != rtd::M_IDLE)) break;
+                if (!__any(L.state != rtd::M_IDLE)) {
+                    // RT_SPEC_SHARE: a wave with nothing left stays as a helper while the block
+                    // has unfinished pixels (their offers may come)
+                    if (!rtd::kSpecShare || rtd::block_active() == 0) break;
+                    __builtin_amdgcn_s_sleep(4);
+                    continue;
+                }
             } else if (!__any(L.pix >= 0)) {
                 break;
             }
@@ -515,7 +529,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     }
     __syncthreads();
     if (threadIdx.x < 8) atomicAdd(&g_mega_seg[threadIdx.x], rt_prof_lds[threadIdx.x]);
-    if (threadIdx.x < 8) atomicAdd(&rtd::g_spec_prof[threadIdx.x], rtd::spec_prof_lds[threadIdx.x]);
+    if (threadIdx.x < 16) atomicAdd(&rtd::g_spec_prof[threadIdx.x], rtd::spec_prof_lds[threadIdx.x]);
 #endif
     rtd::counters_flush<COUNT>(cnt, counters);
 }
@@ -1204,9 +1218,9 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #ifdef RT_MEGA_PROF
             {
-                const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
-                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
+                const unsigned long long z[16] = {};
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_prof), z, 8 * sizeof z[0], 0, hipMemcpyHostToDevice, stream));
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, 8 * sizeof z[0], 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(rtd::g_spec_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
                 static const std::vector<unsigned long long> ztb(kTb * kTbN, 0ull);
@@ -1282,13 +1296,16 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                         }
                     }
                 }
-                unsigned long long sp[8];
+                unsigned long long sp[16];
                 HIP_TRY(hipMemcpyFromSymbolAsync(sp, HIP_SYMBOL(rtd::g_spec_prof), sizeof sp, 0, hipMemcpyDeviceToHost, stream));
                 HIP_TRY(hipStreamSynchronize(stream));
                 std::fprintf(stderr, "[mega prof] runahead: tail waves=%llu passes/tail wave=%.1f cycles/pass=%.0f "
                              "cycles in passes/wave=%.3g frontier jobs=%llu runahead jobs=%llu added=%llu "
                              "runahead jobs proven=%llu invalidations=%llu\n", sp[7], sp[7] ? (double)sp[0] / sp[7] : 0.0,
                              sp[0] ? (double)sp[1] / sp[0] : 0.0, (double)sp[1] / pf[7], sp[2], sp[3], sp[4], sp[5], sp[6]);
+                std::fprintf(stderr, "[mega prof] shared runahead: offers posted=%llu taken=%llu run to the end=%llu "
+                             "added (proven)=%llu reclaimed untaken=%llu cancelled=%llu\n", sp[8], sp[11], sp[9], sp[10],
+                             sp[12], sp[13]);
             }
 #endif
         }

@@ -2,6 +2,7 @@
 // for the host so tests can check its arithmetic against the goldens without a GPU.  Not
 // part of the product: librt_hw_amd.so has no CPU render path.
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 #include <algorithm>
@@ -152,6 +153,9 @@ static int g_static_per_wave = 0;    // > 0: no queue; wave w takes items [w*P, 
 extern "C" void kh_set_static_per_wave(int p) { g_static_per_wave = p; }
 static uint64_t g_rounds = 0;        // main-loop rounds (one iteration of every live wave) of the last render
 extern "C" uint64_t kh_rounds() { return g_rounds; }
+extern "C" void kh_spec_prof(uint64_t *out) {   // the 16 runahead counters (rt_mega.h RT_SPEC_STAT), not reset
+    std::memcpy(out, rtd::g_spec_prof, sizeof rtd::g_spec_prof);
+}
 extern "C" void kh_spec_stats(uint64_t *out) {   // passes, frontier jobs, runahead jobs, added, invalidations
     out[0] = g_spec_passes;
     out[1] = rtd::g_spec_prof[2];
@@ -197,8 +201,34 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     long long queue = 0;
     int live = waves;
     g_rounds = 0;
+    if constexpr (SPEC) {   // blocks of 4 emulated waves: offer boards (RT_SPEC_SHARE)
+        std::memset(rtd::g_spec_board, 0, sizeof rtd::g_spec_board);
+        std::memset(rtd::g_spec_block_active, 0, sizeof rtd::g_spec_block_active);
+        std::memset(rtd::g_spec_fdone, 0, sizeof rtd::g_spec_fdone);
+    }
     while (live > 0) {
         ++g_rounds;
+        if (g_rounds > 50000000ull) {   // (a schedule that stops draining: report, do not hang the test)
+            std::fprintf(stderr, "render_mega: no progress after %llu rounds, %d waves live\n",
+                         (unsigned long long)g_rounds, live);
+            if constexpr (SPEC) {
+                for (int b = 0; b < (waves + 3) / 4; ++b) {
+                    std::fprintf(stderr, " block %d active %d board:", b, rtd::g_spec_block_active[b]);
+                    for (int k = 0; k < rtd::kOffers; ++k) std::fprintf(stderr, " %x", rtd::g_spec_board[b][k * rtd::kOfWords]);
+                    std::fprintf(stderr, "\n");
+                }
+                for (int w = 0; w < waves; ++w) {
+                    const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
+                    for (int l = 0; l < 64; ++l) {
+                        const uint4 a = *V.w(0, l), b = *V.w(1, l), c = *V.w(2, l), d = *V.w(3, l);
+                        if (b.w & rtd::kRecActive)
+                            std::fprintf(stderr, " w%d rec %d: pix %u f %u n %u e %u meta %u tab %08x%08x | lane state %d\n", w, l,
+                                         a.x, a.y, a.z, a.w, b.w, d.w, c.w, lanes[(size_t)w * 64 + l].state);
+                    }
+                }
+            }
+            return -7;
+        }
         for (int w = 0; w < waves; ++w) {
             if (done[w]) continue;
             Lane *W = &lanes[(size_t)w * 64];
@@ -227,8 +257,8 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
             if constexpr (SPEC) {
             if (exhausted[w] && !tail[w]) {
                 const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
-                for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], V, l);
                 rtd::g_mega_slot = (long long)w * 64;
+                for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], V, l);
                 rtd::spec_hint_take();
                 tail[w] = 1;
                 wave_room[w] = 0;
@@ -241,7 +271,9 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                     fresh |= W[l].state == rtd::M_DONE_NEW;
                     idle |= W[l].state == rtd::M_IDLE;
                 }
-                if (fresh || (wave_room[w] && idle)) {
+                bool share_pass = false;
+                if constexpr (rtd::kSpecShare) share_pass = rtd::spec_fdone_take() || (idle && rtd::spec_foreign_open());
+                if (fresh || share_pass || (wave_room[w] && idle)) {
                     ++g_spec_passes;
                     wave_room[w] = rtd::spec_manage(rtd::SpecLanes{W}, sc, g,
                                                     rtd::SpecView{(uint4 *)st.mid, st.lanes, (long long)w * 64}, spp,
@@ -256,7 +288,14 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                 nr += W[l].state == rtd::M_READY || W[l].state == rtd::M_LREADY;
                 nt += W[l].state == rtd::M_TRAV || W[l].state == rtd::M_LTRAV;
             }
-            if (!any) { done[w] = 1; --live; continue; }
+            if (!any) {
+                rtd::g_mega_slot = (long long)w * 64;
+                if constexpr (SPEC && rtd::kSpecShare)
+                    if (tail[w] && rtd::block_active() > 0) continue;   // a helper (RT_SPEC_SHARE)
+                done[w] = 1;
+                --live;
+                continue;
+            }
             const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
             for (int l = 0; l < 64; ++l) {
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
