@@ -352,6 +352,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         for (int k = threadIdx.x; k < rtd::kOffers * rtd::kOfWords; k += blockDim.x) rtd::spec_board()[k] = 0u;
         if (threadIdx.x == 0) rtd::spec_block_active()[0] = 0;
         if (threadIdx.x < 4) rtd::spec_fdone()[threadIdx.x] = 0;
+        if (threadIdx.x < 4) rtd::spec_wave_active_lds[threadIdx.x] = 0;
     }
     __syncthreads();
     DevScene sc = sc_in;
@@ -369,6 +370,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     L.state = rtd::M_IDLE;
     bool exhausted = false;
     bool tail = false, wave_room = false;
+    unsigned idle_checks = 0;   // RT_SPEC_SHARE helpers (below)
     // RT_SPEC_FILL: wave w takes queue items [w * quota, (w + 1) * quota) on lanes 0 .. quota-1
     // (quota = ceil(items / waves), so every item is assigned at once) and no queue is claimed
     if constexpr (kSpec && kSpecFill) {
@@ -382,6 +384,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
     if (threadIdx.x < 16) rtd::spec_prof_lds[threadIdx.x] = 0;
+    if ((threadIdx.x & 63) == 0) rtd::spec_wave_t0_lds[threadIdx.x >> 6] = wall_clock64();
     __syncthreads();
     long long tp = clock64();
     const unsigned long long wt0 = wall_clock64();
@@ -441,11 +444,16 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 }
                 if (!__any(L.state != rtd::M_IDLE)) {
                     // RT_SPEC_SHARE: a wave with nothing left stays as a helper while the block
-                    // has unfinished pixels (their offers may come)
+                    // has unfinished pixels (their offers may come).  A wave whose own records
+                    // are unfinished (all its jobs on the board) always stays; a helper leaves
+                    // after 2^16 idle checks (about 10 ms) without work, so a bug cannot keep a
+                    // launch resident.
                     if (!rtd::kSpecShare || rtd::block_active() == 0) break;
+                    if (rtd::wave_active() == 0 && ++idle_checks > (1u << 16)) break;
                     __builtin_amdgcn_s_sleep(4);
                     continue;
                 }
+                idle_checks = 0;
             } else if (!__any(L.pix >= 0)) {
                 break;
             }
@@ -1306,6 +1314,9 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 std::fprintf(stderr, "[mega prof] shared runahead: offers posted=%llu taken=%llu run to the end=%llu "
                              "added (proven)=%llu reclaimed untaken=%llu cancelled=%llu\n", sp[8], sp[11], sp[9], sp[10],
                              sp[12], sp[13]);
+                std::fprintf(stderr, "[mega prof] runahead chains: proven share of runahead jobs=%.3f, pixels completed "
+                             "in the tail=%llu, mean time per chain link (completion / spp)=%.1f us\n",
+                             sp[3] ? (double)sp[5] / (double)sp[3] : 0.0, sp[15], sp[15] ? (double)sp[14] / sp[15] / 100.0 : 0.0);
             }
 #endif
         }

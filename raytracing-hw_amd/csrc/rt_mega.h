@@ -463,17 +463,26 @@ __device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevSce
 // issued [4] jobs added [5] of them runahead jobs [6] invalidations [7] waves that reached a tail
 // (RT_SPEC_SHARE) [8] offers posted [9] offers run to the end by another wave [10] of them added
 // (proven) [11] offers taken [12] frontier offers reclaimed untaken [13] offers cancelled
+// [14] chain-link time sum (pixel completion since its wave's start / spp) [15] pixels completed
 #if defined(RT_MEGA_PROF) && defined(__HIPCC__)
 // (per-block LDS sums, added to g_spec_prof once at the end of the kernel: global atomics on
 // eight words from every wave serialised the runahead kernel)
 __device__ unsigned long long g_spec_prof[16];
 __shared__ unsigned long long spec_prof_lds[16];
 #define RT_SPEC_STAT(k, v) atomicAdd(&::rtd::spec_prof_lds[k], (unsigned long long)(v))
+// chain links: a pixel's completion time since its wave's start (wall clock, 100 MHz) / spp,
+// summed in [14] (count in [15]); the wave's start time is set by the kernel
+__shared__ unsigned long long spec_wave_t0_lds[4];
+#define RT_SPEC_CHAIN_END(spp) \
+    RT_SPEC_STAT(14, (wall_clock64() - ::rtd::spec_wave_t0_lds[threadIdx.x >> 6]) / (unsigned long long)(spp)); \
+    RT_SPEC_STAT(15, 1)
 #elif !defined(__HIPCC__)
 inline unsigned long long g_spec_prof[16];   // host test harness
 #define RT_SPEC_STAT(k, v) (::rtd::g_spec_prof[k] += (unsigned long long)(v))
+#define RT_SPEC_CHAIN_END(spp) do { } while (0)
 #else
 #define RT_SPEC_STAT(k, v) do { } while (0)
+#define RT_SPEC_CHAIN_END(spp) do { } while (0)
 #endif
 
 // Record meta (plane 1 .w): bit 0 active, bit 1 X_f known (false until the wave's first job of
@@ -547,6 +556,7 @@ constexpr int kOfWords = 14;
 #if defined(__HIPCC__)
 __shared__ uint32_t spec_board_lds[kSpecShare ? kOffers * kOfWords : 1];
 __shared__ int spec_block_active_lds[1];   // unfinished records of the block
+__shared__ int spec_wave_active_lds[4];    // unfinished records of each wave
 __shared__ int spec_fdone_lds[4];          // per wave: a helper finished one of its offers
 __device__ __forceinline__ uint32_t *spec_board() { return spec_board_lds; }
 __device__ __forceinline__ int *spec_block_active() { return spec_block_active_lds; }
@@ -558,12 +568,19 @@ __device__ __forceinline__ bool board_cas(int i, uint32_t expect, uint32_t want)
     return __hip_atomic_compare_exchange_strong(&spec_board()[i], &expect, want, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void block_active_add(int d) { atomicAdd(spec_block_active(), d); }
+__device__ __forceinline__ void block_active_add(int d) {
+    atomicAdd(spec_block_active(), d);
+    atomicAdd(&spec_wave_active_lds[threadIdx.x >> 6], d);
+}
+__device__ __forceinline__ int wave_active() {
+    return __hip_atomic_load(&spec_wave_active_lds[threadIdx.x >> 6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ int block_active() { return __hip_atomic_load(spec_block_active(), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 #else
 // host harness: a board per emulated block (4 waves: mega_slot() / 256)
 inline uint32_t g_spec_board[4096][kOffers * kOfWords];
 inline int g_spec_block_active[4096];
+inline int g_spec_wave_active[4096 * 4];
 inline int g_spec_fdone[4096 * 4];
 inline uint32_t *spec_board() { return g_spec_board[(mega_slot() >> 8) & 4095]; }
 inline int *spec_block_active() { return &g_spec_block_active[(mega_slot() >> 8) & 4095]; }
@@ -576,8 +593,12 @@ inline bool board_cas(int i, uint32_t expect, uint32_t want) {
     spec_board()[i] = want;
     return true;
 }
-inline void block_active_add(int d) { *spec_block_active() += d; }
+inline void block_active_add(int d) {
+    *spec_block_active() += d;
+    g_spec_wave_active[(mega_slot() >> 6) & (4096 * 4 - 1)] += d;
+}
 inline int block_active() { return *spec_block_active(); }
+inline int wave_active() { return g_spec_wave_active[(mega_slot() >> 6) & (4096 * 4 - 1)]; }
 #endif
 __device__ __forceinline__ uint32_t of_state(uint32_t w) { return w & 7u; }
 __device__ __forceinline__ int of_owner(uint32_t w) { return (int)((w >> 16) & 3u); }
@@ -671,15 +692,19 @@ struct SpecLanes {
 
 // Runahead priority (RT_SPEC_PRIO): the order in which records with room in their window get
 // the wave's idle lanes.  0: record (lane) order, which at the tail's start is the pre-pass's
-// heaviest-first order.  1: fewest samples added first (ties by lane): every chain of an 8-way
-// shard starts at the same time, so the chain with the smallest frontier is the one furthest
-// behind (remaining time ~ elapsed x (spp - f) / f), and it is the one that ends the wave.
+// heaviest-first order (rounds 2-4).  1 (default): fewest samples added first (ties by lane):
+// every chain of an 8-way shard starts at the same time, so the chain with the smallest
+// frontier is the one furthest behind (remaining time ~ elapsed x (spp - f) / f), and it is
+// the one that ends the wave.  Round 5 (profiles/r05e_prio_late_ab.jsonl, one box): the 8
+// shards of the 8-way split 186.7-188.5 ms (mean 187.6) against 201.2-205.7 (mean 202.7); the
+// one-GPU frame (plain kernel) is unchanged (1135.0 vs 1136.0 ms); bits unchanged.
 #ifndef RT_SPEC_PRIO
-#define RT_SPEC_PRIO 0
+#define RT_SPEC_PRIO 1
 #endif
 constexpr bool kSpecPrio = RT_SPEC_PRIO != 0;
 // RT_SPEC_LATE=K (A/B): runahead jobs only once at most K records of the wave are unfinished
-// (0: from the tail's start).  Frontier jobs are issued either way.
+// (0: from the tail's start).  Frontier jobs are issued either way.  K = 16: 8-way shards
+// 221.7-230.1 ms against 201.2-205.7 (r05e): the runahead in the full waves pays.
 #ifndef RT_SPEC_LATE
 #define RT_SPEC_LATE 0
 #endif
@@ -837,6 +862,7 @@ __device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const Sh
             *V.w(0, r) = make_uint4(a.x, t + 1u, t + 1u, a.w);
             *V.w(1, r) = v3_pack(sum, 0u);
             if (kSpecShare) block_active_add(-1);
+            RT_SPEC_CHAIN_END(spp);
             L.pix = -1;
             L.state = M_IDLE;
             return;
@@ -965,6 +991,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                     out[o + 2] = sum.z;
                     mm = 0u;
                     if (kSpecShare) block_active_add(-1);
+                    RT_SPEC_CHAIN_END(spp);
                 }
                 rf.put(lane, f);
                 rn.put(lane, n);
@@ -1220,8 +1247,13 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         *V.w(4, lane) = make_uint4(jt.get(lane), y.x, y.saved_avail, __float_as_uint(y.saved));
         const uint32_t m = rm.get(lane);
         const uint32_t f = rf.get(lane), n = rn.get(lane);
-        const bool rm_room = (m & kRecActive) &&
-                             (n == f || (late_ok && (m & kRecXf) && (int)(n - f) < win && (int)n < spp));
+        bool rm_room = (m & kRecActive) &&
+                       (n == f || (late_ok && (m & kRecXf) && (int)(n - f) < win && (int)n < spp));
+        if (kSpecShare && (m & kRecActive) && n > f) {   // a frontier job waiting for a lane, or on the board untaken
+            const int sl0 = (int)(tl.get(lane) & (uint32_t)kTabMask);
+            if (sl0 == kTabNone || (sl0 >= 64 && sl0 < 64 + kOffers && of_state(board_ld((sl0 - 64) * kOfWords)) == kOfOpen))
+                rm_room = true;
+        }
         WBALLOT(roomy, lane, rm_room);
     })
     return roomy != 0;

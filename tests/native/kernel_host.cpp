@@ -204,6 +204,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     if constexpr (SPEC) {   // blocks of 4 emulated waves: offer boards (RT_SPEC_SHARE)
         std::memset(rtd::g_spec_board, 0, sizeof rtd::g_spec_board);
         std::memset(rtd::g_spec_block_active, 0, sizeof rtd::g_spec_block_active);
+        std::memset(rtd::g_spec_wave_active, 0, sizeof rtd::g_spec_wave_active);
         std::memset(rtd::g_spec_fdone, 0, sizeof rtd::g_spec_fdone);
     }
     while (live > 0) {

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--natural", type=int, default=1)
     ap.add_argument("--shard-steps", type=int, default=1)
+    ap.add_argument("--row-block", type=int, default=8, help="rows per interleave block of the N-way split")
+    ap.add_argument("--full", type=int, default=1, help="0: skip the 1-GPU frame (shards only)")
     args = ap.parse_args()
     rt = bench.import_pkg()
     path = bench.load_scenes_module().ensure_scene(args.scene, os.environ.get("RT_SCENE_DIR", "/tmp/rt_scenes"))
@@ -35,16 +37,17 @@ def main():
     scene.upload(0)
     rtdist = __import__("importlib").import_module("raytracing_hw_amd.dist")
     stream = torch.cuda.current_stream().cuda_stream
-    res = {"lib": os.environ.get("RT_LIB", "default")}
+    res = {"lib": os.environ.get("RT_LIB", "default"), "row_block": args.row_block}
 
     import hashlib
     shard_hash = hashlib.sha1()
 
     def t(world, rank, steps, natural):
-        out = torch.zeros(rtdist.max_shard_rows(H, world) * W * 3, dtype=torch.float32, device="cuda")
+        rb = args.row_block if world > 1 else 8
+        out = torch.zeros(rtdist.max_shard_rows(H, world, rb) * W * 3, dtype=torch.float32, device="cuda")
         ms, order = [], []
         for _ in range(steps):
-            st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, stats=True,
+            st = scene.render_device(out.data_ptr(), stream, spp=S, rank=rank, world=world, row_block=rb, stats=True,
                                      natural_order=natural)
             ms.append(st["render_ms"])
             order.append(st["order_ms"])
@@ -53,11 +56,12 @@ def main():
         return min(ms), min(order)
 
     t(1, 0, 1, False)   # warm
-    res["full_ms"], res["full_order_ms"] = t(1, 0, args.steps, False)
-    full = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
-    scene.render_device(full.data_ptr(), stream, spp=S, rank=0, world=1)
-    torch.cuda.synchronize()
-    res["full_sha1"] = __import__("hashlib").sha1(full.cpu().numpy().tobytes()).hexdigest()[:16]
+    if args.full:
+        res["full_ms"], res["full_order_ms"] = t(1, 0, args.steps, False)
+        full = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+        scene.render_device(full.data_ptr(), stream, spp=S, rank=0, world=1)
+        torch.cuda.synchronize()
+        res["full_sha1"] = __import__("hashlib").sha1(full.cpu().numpy().tobytes()).hexdigest()[:16]
     if args.natural:
         res["full_natural_ms"], _ = t(1, 0, args.steps, True)
     sh = [t(args.world, r, args.shard_steps, False)[0] for r in range(args.world)]
