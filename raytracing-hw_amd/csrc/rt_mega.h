@@ -1111,7 +1111,9 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
     if constexpr (kSpecPrio) {
         WArr<uint32_t> key;
         WAVE_PHASE(lane, {
-            key.put(lane, room.get(lane) > 0 ? (rf.get(lane) << 6 | (uint32_t)lane) : (0xffffffc0u | (uint32_t)lane));
+            // (RT_SPEC_PRIO=2, A/B: by the next sample to issue instead of the frontier)
+            const uint32_t lag = RT_SPEC_PRIO == 2 ? rn.get(lane) : rf.get(lane);
+            key.put(lane, room.get(lane) > 0 ? (lag << 6 | (uint32_t)lane) : (0xffffffc0u | (uint32_t)lane));
         })
         wave_order(key, srec, rank);
         WAVE_PHASE(lane, { sroom.put(lane, room.at(srec.get(lane))); })
