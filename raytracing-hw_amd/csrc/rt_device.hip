@@ -150,14 +150,6 @@ constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units 
 #define RT_SPEC_PIXELS_PER_LANE 2
 #endif
 constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
-// Runahead kernel launched on every resident block (RT_SPEC_FILL=1), not just ceil(pixels / 256):
-// a wave's first claim takes at most ceil(pixels / waves) pixels, so where a shard has fewer
-// pixels than resident lanes (an 8-way shard at 5 waves per SIMD) every wave starts with idle
-// lanes for runahead.  0: one lane per pixel, ceil(pixels / 256) blocks.
-#ifndef RT_SPEC_FILL
-#define RT_SPEC_FILL 0
-#endif
-constexpr bool kSpecFill = RT_SPEC_FILL != 0;
 // Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
 // holds at most 64 / k pixels and the grid grows k-fold (lockstep study).
 #ifndef RT_CLAIM_STRIDE
@@ -371,15 +363,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     bool exhausted = false;
     bool tail = false, wave_room = false;
     unsigned idle_checks = 0;   // RT_SPEC_SHARE helpers (below)
-    // RT_SPEC_FILL: wave w takes queue items [w * quota, (w + 1) * quota) on lanes 0 .. quota-1
-    // (quota = ceil(items / waves), so every item is assigned at once) and no queue is claimed
-    if constexpr (kSpec && kSpecFill) {
-        const long long waves = 4LL * gridDim.x, q = (n_items + waves - 1) / waves;
-        const int quota = q < 64 ? (int)q : 64;
-        const long long p = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * quota + lane;
-        if (q <= 64 && lane < quota && p < n_items) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
-        exhausted = q <= 64;   // (more items than lanes: the queue hands out the rest)
-    }
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -1195,11 +1178,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                                     : count ? rt_mega_kernel<true>
                                             : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
             sched = fast ? RT_SCHED_FAST : lsplit ? RT_SCHED_LIGHT_SPLIT : spec ? RT_SCHED_RUNAHEAD : RT_SCHED_LANE;
-            const unsigned blocks = spec && kSpecFill
-                                        ? (unsigned)std::max<long long>(1, std::min<long long>(full_blocks, (n_items + 3) / 4))
-                                        : persistent_blocks(d, mk, n_items * kClaimStride);
-            // the first claim's size per wave (rt_mega_kernel quota), for the spread below
-            const long long first_claim = spec && kSpecFill ? std::min<long long>(64, (n_items + 4LL * blocks - 1) / (4LL * blocks)) : 64;
+            const unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
             const long long slots = (long long)blocks * 256;   // lane slots
             // vertex records are addressed with 32-bit byte offsets (rt_path.h LaneRec)
             if ((unsigned long long)slots * (unsigned long long)s->ray_depth * 32ull >= (1ull << 32))
@@ -1214,7 +1193,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
                 // the spread deals one pixel of every cost stratum to each claim of 64 of the
                 // launch's first round (one per wave)
-                rc = launch_order(d, g, stream, 4LL * blocks, first_claim, &order);
+                rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
                 if (rc) return rc;
                 ordered = true;
             }

@@ -714,13 +714,6 @@ struct SpecLanes {
 #define RT_SPEC_PRIO 1
 #endif
 constexpr bool kSpecPrio = RT_SPEC_PRIO != 0;
-// RT_SPEC_LATE=K (A/B): runahead jobs only once at most K records of the wave are unfinished
-// (0: from the tail's start).  Frontier jobs are issued either way.  K = 16: 8-way shards
-// 221.7-230.1 ms against 201.2-205.7 (r05e): the runahead in the full waves pays.
-#ifndef RT_SPEC_LATE
-#define RT_SPEC_LATE 0
-#endif
-constexpr int kSpecLate = RT_SPEC_LATE;
 
 // srec[k] = the record at position k of the ascending order of key (keys distinct: the lane
 // is in their low 6 bits), rank[r] = the position of record r.  GPU: a bitonic sort over the
@@ -1108,16 +1101,10 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
     // C2. runahead: idle lanes take the next jobs of pixels with room in their window
     WArr<int> room, incl;
     unsigned long long idle2 = 0;
-    bool late_ok = true;
-    if constexpr (kSpecLate > 0) {
-        unsigned long long act = 0;
-        WAVE_PHASE(lane, { WBALLOT(act, lane, (rm.get(lane) & kRecActive) != 0); })
-        late_ok = popc64(act) <= kSpecLate;
-    }
     WAVE_PHASE(lane, {
         int rr = 0;
         const uint32_t m = rm.get(lane);
-        if (late_ok && (m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane) && !spec_gated(m)) {
+        if ((m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane) && !spec_gated(m)) {
             const int w = win - (int)(rn.get(lane) - rf.get(lane)), left = spp - (int)rn.get(lane);
             rr = w < left ? w : left;
             rr = rr < 0 ? 0 : (rr < issue ? rr : issue);
@@ -1270,7 +1257,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         const uint32_t m = rm.get(lane);
         const uint32_t f = rf.get(lane), n = rn.get(lane);
         bool rm_room = (m & kRecActive) &&
-                       (n == f || (late_ok && (m & kRecXf) && !spec_gated(m) && (int)(n - f) < win && (int)n < spp));
+                       (n == f || ((m & kRecXf) && !spec_gated(m) && (int)(n - f) < win && (int)n < spp));
         if (kSpecShare && (m & kRecActive) && n > f) {   // a frontier job waiting for a lane, or on the board untaken
             const int sl0 = (int)(tl.get(lane) & (uint32_t)kTabMask);
             if (sl0 == kTabNone || (sl0 >= 64 && sl0 < 64 + kOffers && of_state(board_ld((sl0 - 64) * kOfWords)) == kOfOpen))
