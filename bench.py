@@ -59,10 +59,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_AABB, B_TRI, B_SHADE = 24, 36, 156
 B_RAY_IO = 24 + 4 + 16     # wf_extend per ray: ray (6 floats) + queue slot in, hit (t, u, v, prim) out
-PROFILE_PREFIX = "r03w"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
+PROFILE_PREFIX = "r05"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
 # profiles/<prefix>_shard_{fetch,write,sq1,sq2}_w<N>.csv: rank 0's shard of the N-way split
 # (tools/pmc_shard.sh), the counters of an --gpus N line
-SHARD_PROFILE_PREFIX = "r04"
+SHARD_PROFILE_PREFIX = "r05"
 # rocprofv3 names of the two parity instantiations of the default kernel: the plain one (one
 # GPU) and the runahead one (shards of at most 2 pixels per lane: the 4- and 8-way splits)
 KERNEL_PLAIN = "void rt_mega_kernel<false, false, false, false>"

@@ -1,19 +1,16 @@
 #!/bin/bash
-# Round-5 call: GPU suite on the default build (runahead priority on), then the A/B of the
-# window, priority and row-block choices, then the block-shared runahead variants (each under
-# a short limit: the first build of it stalled).
+# Round-5 call: GPU suite on the default build (runahead priority on), then one run each of the
+# runahead variants against the default (frame + all 8 shards of the 8-way split, sha1 of both),
+# then the block-shared runahead variant under a short limit (its first build stalled).
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 timeout -k 10 520 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/r05f_gpu_tests.txt 2>&1 \
     || { tail -30 gpurun_out/r05f_gpu_tests.txt; exit 1; }
 tail -2 gpurun_out/r05f_gpu_tests.txt
-REPS=2 bash tools/r05_ab.sh r05f_ab.jsonl default raytracing-hw_amd/v_noprio/librt_hw_amd.so raytracing-hw_amd/v_w4/librt_hw_amd.so || exit 1
-for rb in 4 2 1; do
-  timeout -k 10 150 python3 tools/order_ab.py --natural 0 --full 0 --shard-steps 2 --row-block $rb >> gpurun_out/r05f_ab.jsonl 2>>gpurun_out/r05f_ab.jsonl.err || exit 1
-  tail -1 gpurun_out/r05f_ab.jsonl
-done
-for v in v_share16 v_share64; do
+REPS=1 bash tools/r05_ab.sh r05f_ab.jsonl default raytracing-hw_amd/v_noprio/librt_hw_amd.so raytracing-hw_amd/v_w4/librt_hw_amd.so \
+    raytracing-hw_amd/v_prio2/librt_hw_amd.so raytracing-hw_amd/v_gate30/librt_hw_amd.so raytracing-hw_amd/v_sh48/librt_hw_amd.so default || exit 1
+for v in v_share16; do
   RT_LIB=$PWD/raytracing-hw_amd/$v/librt_hw_amd.so timeout -k 5 100 python3 tools/order_ab.py --natural 0 --full 0 --shard-steps 2 \
       >> gpurun_out/r05f_share.jsonl 2>>gpurun_out/r05f_share.err || { echo "share variant $v failed or stalled"; exit 1; }
   tail -1 gpurun_out/r05f_share.jsonl
