@@ -61,8 +61,10 @@ constexpr int kMegaWpeSpec = RT_SPEC_WPE;
 // Round 3 (window 3): slowest 8-way shard 207.5-207.7 ms at 40 against 208.6-211.7 at 32 and
 // 214.8 at 24, 4-way 346-347 vs 352-354 (profiles/r03_ab.jsonl r03ah, r03ai).  Round 2: 294 ms
 // at 32 against 297-299 at 48 (profiles/r02_tail_ab.jsonl).
+// Round 5, with the runahead priority (rt_mega.h RT_SPEC_PRIO): 48 READY lanes, 8-way shards
+// 187.2 max / 185.6 mean ms against 188.2-188.5 / 186.9-187.5 at 40 (profiles/r05f_prio_variants_ab.jsonl).
 #ifndef RT_SPEC_SHADE_MIN
-#define RT_SPEC_SHADE_MIN 40
+#define RT_SPEC_SHADE_MIN 48
 #endif
 constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
@@ -433,6 +435,26 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                     // launch resident.
                     if (!rtd::kSpecShare || rtd::block_active() == 0) break;
                     if (rtd::wave_active() == 0 && ++idle_checks > (1u << 16)) break;
+#ifdef RT_SHARE_DEBUG
+                    // (diagnostics build: a wave idle this long with its own records unfinished is
+                    // stalled; report its records and the board once, then leave)
+                    if (rtd::wave_active() > 0 && ++idle_checks > (1u << 20)) {
+                        const rtd::SpecView V{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane};
+                        const uint4 a = *V.w(0, lane), b = *V.w(1, lane), c = *V.w(2, lane), d = *V.w(3, lane);
+                        if (lane == 0) {
+                            printf("[share stall] block %d wave %d wave_active %d block_active %d board:", (int)blockIdx.x,
+                                   (int)(threadIdx.x >> 6), rtd::wave_active(), rtd::block_active());
+                            for (int k = 0; k < rtd::kOffers; ++k)
+                                printf(" %x/%u/%u", rtd::spec_board()[k * rtd::kOfWords], rtd::spec_board()[k * rtd::kOfWords + 1],
+                                       rtd::spec_board()[k * rtd::kOfWords + 2]);
+                            printf("\n");
+                        }
+                        if (b.w & rtd::kRecActive)
+                            printf("[share stall]  block %d wave %d rec %d: f %u n %u epoch %u meta %x tab %08x%08x\n",
+                                   (int)blockIdx.x, (int)(threadIdx.x >> 6), lane, a.y, a.z, a.w, b.w, d.w, c.w);
+                        break;
+                    }
+#endif
                     __builtin_amdgcn_s_sleep(4);
                     continue;
                 }
