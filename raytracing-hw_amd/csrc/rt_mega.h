@@ -932,8 +932,10 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         je.put(lane, done ? lane_rng(L) : Rng{0u, 0u, 0.f});
     })
     constexpr int win = kSpecWindow, issue = kSpecIssue;
-    // A. add ended frontier jobs, one per pixel per round, at most `win` rounds
-    for (int q = 0; q < win; ++q) {
+    // A. add ended frontier jobs, one per pixel per round, at most `win` rounds (RT_SPEC_SHARE:
+    // as many as jobs can be in flight, so no finished offer is left waiting for an event)
+    constexpr int rounds = kSpecShare ? kShareWindow : win;
+    for (int q = 0; q < rounds; ++q) {
         WArr<int> prog;
         WAVE_PHASE(lane, {
             const uint32_t m = rm.get(lane);
@@ -1258,10 +1260,15 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         const uint32_t f = rf.get(lane), n = rn.get(lane);
         bool rm_room = (m & kRecActive) &&
                        (n == f || ((m & kRecXf) && !spec_gated(m) && (int)(n - f) < win && (int)n < spp));
-        if (kSpecShare && (m & kRecActive) && n > f) {   // a frontier job waiting for a lane, or on the board untaken
+        if (kSpecShare && (m & kRecActive) && n > f) {
+            // a frontier job waiting for a lane, on the board untaken, or on the board done
+            // (its helper's signal was taken by this pass): the wave needs another pass
             const int sl0 = (int)(tl.get(lane) & (uint32_t)kTabMask);
-            if (sl0 == kTabNone || (sl0 >= 64 && sl0 < 64 + kOffers && of_state(board_ld((sl0 - 64) * kOfWords)) == kOfOpen))
-                rm_room = true;
+            if (sl0 == kTabNone) rm_room = true;
+            if (sl0 >= 64 && sl0 < 64 + kOffers) {
+                const uint32_t st0 = of_state(board_ld((sl0 - 64) * kOfWords));
+                if (st0 == kOfOpen || st0 == kOfDone) rm_room = true;
+            }
         }
         WBALLOT(roomy, lane, rm_room);
     })
