@@ -8,6 +8,9 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 TAG=${1:-r05}
 mkdir -p gpurun_out
+# the rocprofv3 databases are hundreds of MB: keep the CSV summaries only (gpurun merges at most
+# 64 MiB of gpurun_out/ back)
+trap 'find gpurun_out -name "*.db" -delete; find gpurun_out -name "*_results*" -size +1M -delete' EXIT
 timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
     || { tail -5 gpurun_out/${TAG}_bench.err; exit 1; }
 tail -c 300 gpurun_out/${TAG}_bench.json
