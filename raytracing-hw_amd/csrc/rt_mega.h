@@ -502,18 +502,6 @@ inline unsigned long long g_spec_prof[16];   // host test harness
 #endif
 constexpr uint32_t kRecActive = 1u;
 constexpr uint32_t kRecXf = 2u;
-// RT_SPEC_HITGATE=P (A/B, percent; 0 = off): a record whose runahead proved right in fewer than
-// P% of its last links (at least 8 counted; meta bits 8-15 hits, 16-23 links, halved at 255)
-// gets no more runahead jobs: its lanes go to chains whose predictions hold.
-#ifndef RT_SPEC_HITGATE
-#define RT_SPEC_HITGATE 0
-#endif
-constexpr int kSpecHitGate = RT_SPEC_HITGATE;
-__device__ __forceinline__ bool spec_gated(uint32_t m) {
-    if (kSpecHitGate == 0) return false;
-    const uint32_t h = (m >> 8) & 255u, t = (m >> 16) & 255u;
-    return t >= 8u && h * 100u < (uint32_t)kSpecHitGate * t;
-}
 constexpr int kSpecWindow = RT_SPEC_WINDOW;   // jobs in flight per pixel at most, frontier included (<= 10)
 // A runahead job whose sample ends while its pixel's frontier is still running waits for the
 // next pass (M_DONE) instead of triggering one (M_DONE_NEW): its result is only used once the
@@ -971,14 +959,6 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                 unsigned long long tb = tab >> kTabBits;   // table slots 1.. -> 0..
                 const V3 sum = rtv::add(rs.get(lane), c0);
                 const bool keep = (m & kRecXf) && n > f && rng_same(y1, e0);
-                if (kSpecHitGate > 0 && (m & kRecXf) && n > f) {   // a runahead link was tested
-                    uint32_t hh = ((mm >> 8) & 255u) + (keep ? 1u : 0u), tt = ((mm >> 16) & 255u) + 1u;
-                    if (tt == 255u) {
-                        hh >>= 1;
-                        tt >>= 1;
-                    }
-                    mm = (mm & ~0x00ffff00u) | hh << 8 | tt << 16;
-                }
                 RT_SPEC_STAT(5, keep ? 1 : 0);
                 RT_SPEC_STAT(4, 1);
                 if (kSpecShare && off0) {   // the offer's result is used: the slot is free again
@@ -1106,7 +1086,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
     WAVE_PHASE(lane, {
         int rr = 0;
         const uint32_t m = rm.get(lane);
-        if ((m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane) && !spec_gated(m)) {
+        if ((m & kRecActive) && (m & kRecXf) && rn.get(lane) > rf.get(lane)) {
             const int w = win - (int)(rn.get(lane) - rf.get(lane)), left = spp - (int)rn.get(lane);
             rr = w < left ? w : left;
             rr = rr < 0 ? 0 : (rr < issue ? rr : issue);
@@ -1120,9 +1100,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
     if constexpr (kSpecPrio) {
         WArr<uint32_t> key;
         WAVE_PHASE(lane, {
-            // (RT_SPEC_PRIO=2, A/B: by the next sample to issue instead of the frontier)
-            const uint32_t lag = RT_SPEC_PRIO == 2 ? rn.get(lane) : rf.get(lane);
-            key.put(lane, room.get(lane) > 0 ? (lag << 6 | (uint32_t)lane) : (0xffffffc0u | (uint32_t)lane));
+            key.put(lane, room.get(lane) > 0 ? (rf.get(lane) << 6 | (uint32_t)lane) : (0xffffffc0u | (uint32_t)lane));
         })
         wave_order(key, srec, rank);
         WAVE_PHASE(lane, { sroom.put(lane, room.at(srec.get(lane))); })
@@ -1259,7 +1237,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         const uint32_t m = rm.get(lane);
         const uint32_t f = rf.get(lane), n = rn.get(lane);
         bool rm_room = (m & kRecActive) &&
-                       (n == f || ((m & kRecXf) && !spec_gated(m) && (int)(n - f) < win && (int)n < spp));
+                       (n == f || ((m & kRecXf) && (int)(n - f) < win && (int)n < spp));
         if (kSpecShare && (m & kRecActive) && n > f) {
             // a frontier job waiting for a lane, on the board untaken, or on the board done
             // (its helper's signal was taken by this pass): the wave needs another pass
