@@ -15,3 +15,5 @@ done
 unset RT_LIB
 timeout -k 10 150 python3 tools/order_ab.py --natural 1 --full 1 --steps 1 --shard-steps 1 >> $out 2>>$out.err || exit 1
 tail -1 $out
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05i_smoke.txt 2>&1 || { tail -5 gpurun_out/r05i_smoke.txt; exit 1; }
+tail -1 gpurun_out/r05i_smoke.txt
