@@ -136,6 +136,9 @@ constexpr int kCoopRoundNodes = 4096;
 #ifndef RT_ORDER_SNAKE
 #define RT_ORDER_SNAKE 0
 #endif
+#ifndef RT_ORDER_NOSPREAD
+#define RT_ORDER_NOSPREAD 0
+#endif
 constexpr int kOrderSpp = RT_ORDER_SPP;       // samples per pixel of the counting pre-pass
 constexpr int kOrderRadius = RT_ORDER_RADIUS;  // box filter of the pre-pass costs ((2r+1)^2 pixels)
 // The pre-pass and sort cost about one sample per pixel, so below kOrderMinSpp the order
@@ -595,7 +598,9 @@ __global__ void __launch_bounds__(256) rt_order_spread_kernel(const int *sorted,
     long long r = q;
     if (q < m) {
         const long long gi = q / per, j = q % per, a = m / per, b = m % per;
-#if RT_ORDER_SNAKE
+#if RT_ORDER_NOSPREAD
+        r = q;   // (A/B: heaviest first, no spread: a wave's pixels are of one cost stratum)
+#elif RT_ORDER_SNAKE
         // (A/B: odd strata dealt in reverse, so the wave holding a stratum's heaviest pixel
         // gets the next stratum's lightest)
         const long long size = a + (j < b ? 1 : 0);
