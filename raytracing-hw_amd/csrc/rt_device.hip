@@ -75,6 +75,10 @@ constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes 
 #define RT_INNER_TRAV 1
 #endif
 constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
+#ifndef RT_INV_RECOMPUTE
+#define RT_INV_RECOMPUTE 0
+#endif
+constexpr bool kInvRecompute = RT_INV_RECOMPUTE != 0;
 // The lane-resident kernel's traversal state shares the node and leaf fields (rt_wavefront.h
 // TravStateU; the runahead kernel keeps TravState).  0: TravState everywhere, for A/B builds.
 #ifndef RT_PLAIN_TRAV_SHARED
@@ -523,6 +527,10 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         } else {
             rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
                                                                                root, S, nodes, cnt, kSpec && tail);
+            // RT_INV_RECOMPUTE (A/B): 1 / direction is recomputed after a shading pass (the same
+            // IEEE division as make_ray, so the same bits), so a traversing lane does not hold it
+            // through the pass's register peak
+            if (kInvRecompute && shade_now) L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
         }
 #ifdef RT_MEGA_PROF
         {
