@@ -231,11 +231,21 @@ __device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const Shar
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
                                            Counters &cnt, bool tail = false) {
     LaneRec P{st.rec_ab, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
-    const Hit h = L.T.best;
+    Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
     bool next = false;
     const bool shaded = h.prim >= 0 && h.t < sc.max_distance;
     if (shaded) {
+#if defined(__HIPCC__)
+        if constexpr (kUvRecompute) {   // (u, v) of the closest hit (rt_wavefront.h RT_UV_RECOMPUTE)
+            const float4 *t = sc.tri + 3 * (size_t)h.prim;
+            const float4 t0 = t[0], t1 = t[1], t2 = t[2];
+            TriHit th;
+            tri_hit_bl(V3{t0.x, t0.y, t0.z}, V3{t0.w, t1.x, t1.y}, V3{t1.z, t1.w, t2.x}, L.r, th);
+            h.u = th.u;
+            h.v = th.v;
+        }
+#endif
         Rng rng = lane_rng(L);
         const bool cont = shade_hit<COUNT>(sc, L.r, h, rng, cnt, P, c.nv, stk);   // (stack free: T.sp == 0)
         lane_rng_set(L, rng);

@@ -581,18 +581,29 @@ struct LdsStackT {
 #define RT_SOA 0   // 1: SoA node / triangle planes for the coop step (A/B build)
 #endif
 
+// RT_UV_RECOMPUTE (A/B): the coop leaf step keeps only (t, triangle) of the closest hit; the
+// shading pass recomputes (u, v) with the same Moller-Trumbore test of that triangle and ray
+// (rt_mega.h mega_shade: same inputs, same operations, same bits), so a traversing lane holds
+// two registers fewer through the whole loop and the quad reduction moves two values fewer.
+#ifndef RT_UV_RECOMPUTE
+#define RT_UV_RECOMPUTE 0
+#endif
+constexpr bool kUvRecompute = RT_UV_RECOMPUTE != 0;
+
 // One step of the quad reduction: take the partner lane's (t, u, v, index) when its t is
 // less, or equal with a lower index.
 template <int CTL>
 __device__ __forceinline__ void quad_min_step(float &c, float &cu, float &cv, int &cj) {
     const float c2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(c), CTL, 0xF, 0xF, false));
-    const float u2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cu), CTL, 0xF, 0xF, false));
-    const float v2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cv), CTL, 0xF, 0xF, false));
     const int j2 = __builtin_amdgcn_mov_dpp(cj, CTL, 0xF, 0xF, false);
     const bool take = c2 < c || (c2 == c && j2 < cj);
+    if (!kUvRecompute) {
+        const float u2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cu), CTL, 0xF, 0xF, false));
+        const float v2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cv), CTL, 0xF, 0xF, false));
+        cu = take ? u2 : cu;
+        cv = take ? v2 : cv;
+    }
     c = take ? c2 : c;
-    cu = take ? u2 : cu;
-    cv = take ? v2 : cv;
     cj = take ? j2 : cj;
 }
 
@@ -704,15 +715,18 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
         quad_min_step<0xB1>(c, cu, cv, cj);   // quad_perm [1,0,3,2]: lane ^ 1
         quad_min_step<0x4E>(c, cu, cv, cj);   // quad_perm [2,3,0,1]: lane ^ 2
         const int src = 4 * (served ? rank : 0);
-        const float wc = __shfl(c, src, 64), wu = __shfl(cu, src, 64), wv = __shfl(cv, src, 64);
+        const float wc = __shfl(c, src, 64);
+        const float wu = kUvRecompute ? 0.f : __shfl(cu, src, 64), wv = kUvRecompute ? 0.f : __shfl(cv, src, 64);
         const int wj = __shfl(cj, src, 64);
         if (served) {
             if (COUNT) cnt.tri += (T.kend - T.k < 4u ? T.kend - T.k : 4u);
             if (wc < T.acc) T.acc = wc;
             if (wc < T.best.t) {
                 T.best.t = wc;
-                T.best.u = wu;
-                T.best.v = wv;
+                if (!kUvRecompute) {
+                    T.best.u = wu;
+                    T.best.v = wv;
+                }
                 T.best.prim = (int)(T.k + (uint32_t)wj);
             }
             T.k += 4u;
