@@ -76,7 +76,7 @@ constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes 
 #endif
 constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #ifndef RT_INV_RECOMPUTE
-#define RT_INV_RECOMPUTE 0
+#define RT_INV_RECOMPUTE 1
 #endif
 constexpr bool kInvRecompute = RT_INV_RECOMPUTE != 0;
 // The lane-resident kernel's traversal state shares the node and leaf fields (rt_wavefront.h
@@ -527,9 +527,10 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         } else {
             rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
                                                                                root, S, nodes, cnt, kSpec && tail);
-            // RT_INV_RECOMPUTE (A/B): 1 / direction is recomputed after a shading pass (the same
-            // IEEE division as make_ray, so the same bits), so a traversing lane does not hold it
-            // through the pass's register peak
+            // RT_INV_RECOMPUTE: 1 / direction is recomputed after a shading pass (the same IEEE
+            // division as make_ray, so the same bits), so a traversing lane does not hold it
+            // through the pass's register peak (plain kernel 48 -> 42 spilled VGPRs; 39 with
+            // RT_UV_RECOMPUTE; frame -1.5% alone, -2.6% with it: profiles/r05k_ab.jsonl).  0: A/B.
             if (kInvRecompute && shade_now) L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
         }
 #ifdef RT_MEGA_PROF

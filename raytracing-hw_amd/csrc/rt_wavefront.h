@@ -581,12 +581,14 @@ struct LdsStackT {
 #define RT_SOA 0   // 1: SoA node / triangle planes for the coop step (A/B build)
 #endif
 
-// RT_UV_RECOMPUTE (A/B): the coop leaf step keeps only (t, triangle) of the closest hit; the
+// RT_UV_RECOMPUTE: the coop leaf step keeps only (t, triangle) of the closest hit; the
 // shading pass recomputes (u, v) with the same Moller-Trumbore test of that triangle and ray
 // (rt_mega.h mega_shade: same inputs, same operations, same bits), so a traversing lane holds
 // two registers fewer through the whole loop and the quad reduction moves two values fewer.
+// Round 5 (profiles/r05k_ab.jsonl, with RT_INV_RECOMPUTE): frame 1104-1107 ms vs 1132-1137,
+// 8-way shards 184.6 vs 187.0-187.8 ms, WRITE_SIZE 0.372 vs 0.457 TB per frame.  0: A/B.
 #ifndef RT_UV_RECOMPUTE
-#define RT_UV_RECOMPUTE 0
+#define RT_UV_RECOMPUTE 1
 #endif
 constexpr bool kUvRecompute = RT_UV_RECOMPUTE != 0;
 
