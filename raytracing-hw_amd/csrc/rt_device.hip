@@ -75,6 +75,10 @@ constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes 
 #define RT_INNER_TRAV 1
 #endif
 constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
+#ifndef RT_PACK_TRAV
+#define RT_PACK_TRAV 0
+#endif
+constexpr bool kPackTrav = RT_PACK_TRAV != 0;
 #ifndef RT_INV_RECOMPUTE
 #define RT_INV_RECOMPUTE 1
 #endif
@@ -524,6 +528,21 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 tbk.c[2] += (unsigned long long)__popcll(__ballot(L.state != rtd::M_IDLE));
 #endif
             } while (true);
+        } else if (kPackTrav && kInnerTrav && !LSPLIT && !kSpec && !FAST) {
+            // shading pass (the inner loop above runs every traversal iteration): a lane that
+            // does not shade keeps its phase, stack depth and state packed in one register
+            // through the pass (RT_PACK_TRAV)
+            uint32_t pk = (uint32_t)L.T.phase | (uint32_t)L.state << 2 | (uint32_t)L.T.sp << 5;
+            asm volatile("" : "+v"(pk));
+            if (L.state == rtd::M_READY) {
+                L.T.phase = 0;   // dead in a READY lane (its stack is empty: T.sp == 0)
+                L.T.sp = 0;
+                rtd::mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, S, cnt);
+            } else {
+                L.T.phase = (int)(pk & 3u);
+                L.state = (int)((pk >> 2) & 7u);
+                L.T.sp = (int)(pk >> 5);
+            }
         } else {
             rtd::mega_iterate<COUNT, decltype(S), decltype(nodes), FAST, LSPLIT>(L, shade_now, sc, g, st, spp, out, cost,
                                                                                root, S, nodes, cnt, kSpec && tail);
@@ -533,6 +552,8 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             // RT_UV_RECOMPUTE; frame -1.5% alone, -2.6% with it: profiles/r05k_ab.jsonl).  0: A/B.
             if (kInvRecompute && shade_now) L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
         }
+        if (kPackTrav && kInvRecompute && kInnerTrav && !LSPLIT && !kSpec && !FAST && shade_now)
+            L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
