@@ -373,6 +373,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     std::conditional_t<kSpec || !kPlainTravShared, rtd::MegaLane, rtd::MegaLaneU> L;
     L.pix = -1;
     L.state = rtd::M_IDLE;
+    L.wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x) & ~63u;
     bool exhausted = false;
     bool tail = false, wave_room = false;
     unsigned idle_checks = 0;   // RT_SPEC_SHARE helpers (below)
@@ -393,11 +394,13 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             if (m) {
                 const int leader = __ffsll((unsigned long long)m) - 1;
                 const unsigned cm = (unsigned)__popcll(m);
+                // claiming lanes below this one (mbcnt of the ballot: no per-lane mask held)
+                const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(queue, (unsigned long long)cm);
+                if (need && below == 0) base = atomicAdd(queue, (unsigned long long)cm);   // the leader
                 base = __shfl(base, leader, 64);
                 if (need) {
-                    const long long p = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
+                    const long long p = (long long)base + below;
                     if (p < n_items) {
                         if (FAST) rtd::mega_assign_fast<COUNT>(L, sc, g, p, cs, spp, root, cnt);
                         else rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
@@ -982,6 +985,8 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.max_distance = s->max_distance;
     ds.width = s->width;
     ds.height = s->height;
+    ds.fwidth = (float)s->width;
+    ds.fheight = (float)s->height;
     std::memcpy(ds.cam_pos, s->cam_pos, sizeof ds.cam_pos);
     std::memcpy(ds.cam_axes, s->cam_axes, sizeof ds.cam_axes);
     std::memcpy(ds.tan_fov, s->tan_half_fov, sizeof ds.tan_fov);
@@ -1188,7 +1193,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
         return rt_fail(RT_ERR_LIMIT, "rt_render: frames above 2^31 pixels are not supported");
     const int64_t rows = rt_shard_rows_impl(s->height, rank, world, rb, nullptr);
     if (rows < 0) return RT_ERR_ARG;
-    ShardGeom g{s->width, rank, world, rb, (long long)rows * s->width};
+    const ShardGeom g = rtd::shard_geom(s->width, rank, world, rb, (long long)rows * s->width);
     rt_device_scene *d = s->dev[p->device];
     DeviceGuard guard(d->device);
     if (!guard.ok) return rt_fail(RT_ERR_DEVICE, "hipSetDevice failed");

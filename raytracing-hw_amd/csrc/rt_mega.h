@@ -54,6 +54,7 @@ struct MegaLaneT {
     V3 sum;
     Ray r;
     TS T;
+    uint32_t wbase;   // threadIdx.x of the wave's lane 0 (uniform: an SGPR; RT_TID_REMAT)
 };
 // The runahead kernel's lanes (and the host harness's spec emulation) keep TravState; the
 // lane-resident kernel's TravStateU (rt_wavefront.h).
@@ -64,20 +65,45 @@ using MegaLaneU = MegaLaneT<TravStateU>;
 // through the shading code; with the RNG state below in LDS too: 30 -> 17 spilled VGPRs at
 // the 96-VGPR budget, 1478 -> 1517 Mrays/s at 1080p x256spp, 8-way shard 325 -> 318 ms.
 #if defined(__HIPCC__)
+// RT_TID_REMAT: the lane's index in its block is recomputed where it is used (the wave's base
+// in an SGPR | mbcnt), not held: the compiler computes threadIdx-based LDS addresses and slot
+// indices once at kernel entry and keeps them, per lane, in VGPRs through the whole kernel
+// (spilled, as loop invariants, at the register peak of the shading pass).  The mbcnt pair is
+// in a volatile asm so that it is neither hoisted nor merged.
+#ifndef RT_TID_REMAT
+#define RT_TID_REMAT 0
+#endif
+constexpr bool kTidRemat = RT_TID_REMAT != 0;
+__device__ __forceinline__ uint32_t lane_id_fresh() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+template <class ML>
+__device__ __forceinline__ int lane_tid(const ML &L) {
+    if constexpr (kTidRemat) return (int)(L.wbase | lane_id_fresh());
+    else return (int)threadIdx.x;
+}
+template <class ML>
+__device__ __forceinline__ long long mega_slot_of(const ML &L) {
+    return (long long)blockIdx.x * blockDim.x + lane_tid(L);
+}
 __shared__ float mega_lds_sum[3 * 256];
 template <class ML>
-__device__ __forceinline__ V3 lane_sum(const ML &) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ V3 lane_sum(const ML &L) {
+    const int t = lane_tid(L);
     return V3{mega_lds_sum[t], mega_lds_sum[256 + t], mega_lds_sum[512 + t]};
 }
 template <class ML>
-__device__ __forceinline__ void lane_sum_set(ML &, V3 v) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ void lane_sum_set(ML &L, V3 v) {
+    const int t = lane_tid(L);
     mega_lds_sum[t] = v.x;
     mega_lds_sum[256 + t] = v.y;
     mega_lds_sum[512 + t] = v.z;
 }
 #else
+template <class ML>
+inline long long mega_slot_of(const ML &) { return mega_slot(); }
 template <class ML>
 __device__ __forceinline__ V3 lane_sum(const ML &L) { return L.sum; }
 template <class ML>
@@ -97,16 +123,16 @@ __device__ __forceinline__ void rng_word_unpack(uint32_t w, uint32_t &x, uint32_
 #if defined(__HIPCC__)
 __shared__ uint32_t mega_lds_rng[2 * 256];
 template <class ML>
-__device__ __forceinline__ Rng lane_rng(const ML &) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ Rng lane_rng(const ML &L) {
+    const int t = lane_tid(L);
     Rng r;
     rng_word_unpack(mega_lds_rng[t], r.x, r.saved_avail);
     r.saved = __uint_as_float(mega_lds_rng[256 + t]);
     return r;
 }
 template <class ML>
-__device__ __forceinline__ void lane_rng_set(ML &, const Rng &r) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ void lane_rng_set(ML &L, const Rng &r) {
+    const int t = lane_tid(L);
     mega_lds_rng[t] = rng_word_pack(r.x, r.saved_avail);
     mega_lds_rng[256 + t] = __float_as_uint(r.saved);
 }
@@ -149,7 +175,8 @@ __device__ __forceinline__ void mega_sample(ML &L, const DevScene &sc, const Sha
     LaneCtr c = lane_ctr(L);
     Rng rng = FAST ? Rng{fast_sample_seed(L.gpix, (uint32_t)c.s), 0u, 0.f} : lane_rng(L);
     {   // start_sample (rt_wavefront.h) with 32-bit pixel arithmetic
-        const int k = L.pix / g.width, px = L.pix - k * g.width, py = shard_row(g, k);
+        int px, py;
+        shard_xy(g, L.pix, px, py);
         const float ox = rng_offset(rng);
         const float oy = rng_offset(rng);
         c.power = sc.ray_depth - 1;
@@ -169,7 +196,8 @@ __device__ __forceinline__ void mega_assign(ML &L, const DevScene &sc, const Sha
     lane_ctr_set(L, LaneCtr{0, 0, 0});
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
     L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
-    const int k = p / g.width, px = p - k * g.width, py = shard_row(g, k);
+    int px, py;
+    shard_xy(g, p, px, py);
     const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
     lane_rng_set(L, Rng{seed == 0 ? 1u : seed, 0u, 0.f});
     mega_sample<COUNT>(L, sc, g, root, cnt);
@@ -190,7 +218,8 @@ __device__ __forceinline__ void mega_assign_fast(ML &L, const DevScene &sc, cons
     L.send = s0 + cs < spp ? s0 + cs : spp;
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
     L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
-    const int k = p / g.width, px = p - k * g.width, py = shard_row(g, k);
+    int px, py;
+    shard_xy(g, p, px, py);
     L.gpix = (uint32_t)(py * sc.width + px);
     mega_sample<COUNT, true>(L, sc, g, root, cnt);
 }
@@ -230,7 +259,7 @@ template <bool COUNT, bool FAST = false, class Stack, class ML>
 __device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
                                            Counters &cnt, bool tail = false) {
-    LaneRec P{st.rec_ab, st.rec_c, mega_slot(), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
+    LaneRec P{st.rec_ab, st.rec_c, mega_slot_of(L), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
     bool next = false;

@@ -131,6 +131,8 @@ struct DevScene {
     int ray_depth;
     float max_distance;
     int width, height;
+    float fwidth, fheight;   // (float)width, (float)height: kernel arguments, so the camera
+                             // ray's divisions take them from SGPRs (no per-lane copy)
     float cam_pos[3];
     float cam_axes[9];
     float tan_fov[2];
@@ -1060,8 +1062,8 @@ __device__ V3 trace_sample(const DevScene &sc, Ray r, Rng &rng, Counters &cnt) {
 // Camera::cast_in_pixel (camera.cpp:49-62)
 __device__ __forceinline__ Ray camera_ray(const DevScene &sc, int px, int py, float ox, float oy) {
     V3 t;
-    t.x = (2.f * ((float)px + 0.5f + ox) / (float)sc.width - 1) * sc.tan_fov[0];
-    t.y = -(2.f * ((float)py + 0.5f + oy) / (float)sc.height - 1) * sc.tan_fov[1];
+    t.x = (2.f * ((float)px + 0.5f + ox) / sc.fwidth - 1) * sc.tan_fov[0];
+    t.y = -(2.f * ((float)py + 0.5f + oy) / sc.fheight - 1) * sc.tan_fov[1];
     t.z = 1;
     V3 d{0.f, 0.f, 0.f};
     const float tv[3] = {t.x, t.y, t.z};

@@ -20,13 +20,43 @@ namespace rtd {
 
 // Pixel-row shard geometry (include/rt_hw.h rt_params): the k-th owned row of rank r is
 // the k-th row whose (row / row_block) % world == rank.
+// Pixel p of the shard is (p % width, shard_row(p / width)).  The two divisions by uniform
+// divisors run as multiply-and-shift with host-made constants (div_magic): with a plain `/`
+// the compiler computes the divisor's reciprocal on the VALU once and holds it, per lane, in
+// a VGPR through the whole lane-resident kernel (two of its spilled VGPRs).
 struct ShardGeom {
     int width, rank, world, row_block;
     long long n_pixels;
+    uint32_t wm, rbm;   // div_magic constants of width and row_block (shard_geom)
+    int ws, rbs;
 };
+// n / d for 0 <= n < 2^31 and d >= 1 (Granlund-Montgomery with N = 31: l = ceil(log2 d),
+// m = ceil(2^(31 + l) / d) < 2^32, s = 31 + l; exact for every such n).  Pixel indices and
+// shard rows are below 2^31 (the host rejects larger frames).
+__device__ __forceinline__ int div_magic(int n, uint32_t m, int s) {
+    return (int)(((unsigned long long)(uint32_t)n * m) >> s);
+}
+inline void div_magic_make(uint32_t d, uint32_t &m, int &s) {
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    s = 31 + l;
+    m = (uint32_t)(((1ull << s) + d - 1) / d);
+}
+inline ShardGeom shard_geom(int width, int rank, int world, int row_block, long long n_pixels) {
+    ShardGeom g{width, rank, world, row_block, n_pixels, 0u, 0u, 0, 0};
+    div_magic_make((uint32_t)width, g.wm, g.ws);
+    div_magic_make((uint32_t)row_block, g.rbm, g.rbs);
+    return g;
+}
 __device__ __forceinline__ int shard_row(const ShardGeom &g, int k) {
-    const int blk = k / g.row_block;
-    return (blk * g.world + g.rank) * g.row_block + (k % g.row_block);
+    const int blk = div_magic(k, g.rbm, g.rbs);
+    return (blk * g.world + g.rank) * g.row_block + (k - blk * g.row_block);
+}
+// Column and frame row of shard pixel p.
+__device__ __forceinline__ void shard_xy(const ShardGeom &g, long long p, int &px, int &py) {
+    const int k = div_magic((int)p, g.wm, g.ws);
+    px = (int)p - k * g.width;
+    py = shard_row(g, k);
 }
 
 struct WfState {
@@ -765,7 +795,8 @@ __device__ __forceinline__ void closest_hit_wf(const DevScene &sc, const float4 
 // Start sample s of slot i: jittered camera ray (scene.cpp:36-39); the first traversal
 // consumes one call of the depth budget (scene.cpp:72-75).
 __device__ __forceinline__ Ray start_sample(const DevScene &sc, const ShardGeom &g, long long i, Rng &rng, int &power) {
-    const int k = (int)(i / g.width), px = (int)(i % g.width), py = shard_row(g, k);
+    int px, py;
+    shard_xy(g, i, px, py);
     const float ox = rng_offset(rng);
     const float oy = rng_offset(rng);
     power = sc.ray_depth - 1;
@@ -779,7 +810,8 @@ __device__ __forceinline__ Ray start_sample(const DevScene &sc, const ShardGeom 
 // wf_init: seed slot i's RNG from its pixel (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1)
 // and start its first sample; returns the camera ray.
 __device__ __forceinline__ Ray wf_init_slot(const DevScene &sc, const ShardGeom &g, const WfState &st, long long i) {
-    const int k = (int)(i / g.width), px = (int)(i % g.width), py = shard_row(g, k);
+    int px, py;
+    shard_xy(g, i, px, py);
     const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
     Rng rng{seed == 0 ? 1u : seed, 0u, 0.f};
     int power = 0;

@@ -39,6 +39,8 @@ static rtd::DevScene make(const rt_scene_view *v) {
     s.max_distance = v->max_distance;
     s.width = v->width;
     s.height = v->height;
+    s.fwidth = (float)v->width;
+    s.fheight = (float)v->height;
     std::memcpy(s.cam_pos, v->cam_pos, sizeof s.cam_pos);
     std::memcpy(s.cam_axes, v->cam_axes, sizeof s.cam_axes);
     std::memcpy(s.tan_fov, v->tan_half_fov, sizeof s.tan_fov);
@@ -72,7 +74,7 @@ extern "C" int kh_render_wf(const rt_scene_view *v, int spp, int rank, int world
     for (int r = 0; r < v->height; ++r)
         if ((r / row_block) % world == rank) ++rows;
     const long long n = (long long)rows * v->width;
-    rtd::ShardGeom g{v->width, rank, world, row_block, n};
+    const rtd::ShardGeom g = rtd::shard_geom(v->width, rank, world, row_block, n);
     const int D = v->ray_depth;
     std::vector<float4> stv((size_t)2 * n), ab((size_t)2 * n * D);
     std::vector<float> cv((size_t)n * D);
@@ -151,6 +153,31 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
 static uint64_t g_spec_passes = 0;   // management passes since the last kh_spec_stats
 static int g_static_per_wave = 0;    // > 0: no queue; wave w takes items [w*P, w*P+P) (study of spare lanes)
 extern "C" void kh_set_static_per_wave(int p) { g_static_per_wave = p; }
+// div_magic (rt_wavefront.h) against `/` for divisor d: every n below 2^20, the 2^20 values
+// below 2^31, the multiples of d and their neighbours up to 2^31, and `extra` seeded draws;
+// returns the number of mismatches.
+extern "C" int64_t kh_div_magic_check(uint32_t d, uint32_t extra) {
+    uint32_t m = 0;
+    int sh = 0;
+    rtd::div_magic_make(d, m, sh);
+    int64_t bad = 0;
+    auto chk = [&](uint64_t n) {
+        if (n < (1ull << 31) && (uint64_t)rtd::div_magic((int)n, m, sh) != n / d) ++bad;
+    };
+    for (uint64_t n = 0; n < (1u << 20); ++n) chk(n);
+    for (uint64_t n = (1ull << 31) - (1u << 20); n < (1ull << 31); ++n) chk(n);
+    for (uint64_t q = 1; q * d < (1ull << 31) + d && q < (1u << 22); ++q) {
+        chk(q * d - 1);
+        chk(q * d);
+    }
+    uint64_t x = 0x9e3779b97f4a7c15ull ^ d;
+    for (uint32_t i = 0; i < extra; ++i) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        chk(x & 0x7fffffffu);
+    }
+    return bad;
+}
+
 static uint64_t g_rounds = 0;        // main-loop rounds (one iteration of every live wave) of the last render
 extern "C" uint64_t kh_rounds() { return g_rounds; }
 extern "C" void kh_spec_prof(uint64_t *out) {   // the 16 runahead counters (rt_mega.h RT_SPEC_STAT), not reset
@@ -176,7 +203,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     for (int r = 0; r < v->height; ++r)
         if ((r / row_block) % world == rank) ++rows;
     const long long n = (long long)rows * v->width;
-    rtd::ShardGeom g{v->width, rank, world, row_block, n};
+    const rtd::ShardGeom g = rtd::shard_geom(v->width, rank, world, row_block, n);
     const int D = v->ray_depth;
     const long long slots = std::max<long long>(n, (long long)waves * 64);
     std::vector<float4> ab((size_t)2 * slots * D);

@@ -41,6 +41,8 @@ def _build_kh(tmp_path_factory, *defines):
     lib.kh_box_pair_check.restype = ctypes.c_int64
     lib.kh_decode_check.argtypes = []
     lib.kh_decode_check.restype = ctypes.c_int64
+    lib.kh_div_magic_check.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    lib.kh_div_magic_check.restype = ctypes.c_int64
     return lib
 
 
@@ -401,3 +403,12 @@ def test_linear_texel_decode_and_rng_word(kh):
     flag in one LDS word) round-trips.  The device runs the same checks
     (rt_device_selfcheck 1, tests/test_gpu_parity.py)."""
     assert kh.kh_decode_check() == 0
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 8, 33, 64, 255, 256, 1000, 1023, 1024, 1025, 1920, 3840, 7680,
+                               65535, 65536, 99991, (1 << 30) - 1, 1 << 30, (1 << 30) + 1, (1 << 31) - 1])
+def test_div_magic_matches_division(kh, d):
+    """The kernels' pixel -> (column, shard row) divisions (rt_wavefront.h div_magic: multiply
+    and shift with host-made constants) equal integer division for every n < 2^31 they can see:
+    all small n, the top 2^20, every multiple of d and its predecessor, and 2^20 seeded draws."""
+    assert kh.kh_div_magic_check(d, 1 << 20) == 0
