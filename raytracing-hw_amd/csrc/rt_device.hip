@@ -75,8 +75,13 @@ constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes 
 #define RT_INNER_TRAV 1
 #endif
 constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
+// RT_PACK_TRAV: through a shading pass, a lane that does not shade holds its traversal phase,
+// stack depth and state packed in one register (the loop body below).  With RT_TID_REMAT
+// (rt_mega.h) the plain kernel spills 16 VGPRs instead of 33 and writes 0.11 instead of
+// 0.37 TB per frame (WRITE_SIZE: 53 instead of 178 B per ray); frame 1038-1041 ms against
+// 1093-1094 (profiles/r05n_ab.jsonl).  0: A/B.
 #ifndef RT_PACK_TRAV
-#define RT_PACK_TRAV 0
+#define RT_PACK_TRAV 1
 #endif
 constexpr bool kPackTrav = RT_PACK_TRAV != 0;
 #ifndef RT_INV_RECOMPUTE
@@ -373,6 +378,12 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     std::conditional_t<kSpec || !kPlainTravShared, rtd::MegaLane, rtd::MegaLaneU> L;
     L.pix = -1;
     L.state = rtd::M_IDLE;
+    // A lane that never gets a pixel still takes part in the shading pass's packing
+    // (RT_PACK_TRAV: phase | state << 2 | sp << 5): its phase and stack depth are defined from
+    // the start, not the register contents the previous kernel left (a stray phase bit would
+    // turn an idle lane's state into TRAV or READY).
+    L.T.phase = rtd::TP_POP;
+    L.T.sp = 0;
     L.wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x) & ~63u;
     bool exhausted = false;
     bool tail = false, wave_room = false;
@@ -535,6 +546,8 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             // shading pass (the inner loop above runs every traversal iteration): a lane that
             // does not shade keeps its phase, stack depth and state packed in one register
             // through the pass (RT_PACK_TRAV)
+            // (phase < 4, state < 8 and sp <= kStack in every lane: all three are set at the
+            // kernel's start and only ever assigned those values)
             uint32_t pk = (uint32_t)L.T.phase | (uint32_t)L.state << 2 | (uint32_t)L.T.sp << 5;
             asm volatile("" : "+v"(pk));
             if (L.state == rtd::M_READY) {

@@ -71,7 +71,7 @@ using MegaLaneU = MegaLaneT<TravStateU>;
 // (spilled, as loop invariants, at the register peak of the shading pass).  The mbcnt pair is
 // in a volatile asm so that it is neither hoisted nor merged.
 #ifndef RT_TID_REMAT
-#define RT_TID_REMAT 0
+#define RT_TID_REMAT 1   // 0: A/B (profiles/r05n_ab.jsonl: 1074.9-1078.9 ms alone, 1037.9-1040.6 with RT_PACK_TRAV)
 #endif
 constexpr bool kTidRemat = RT_TID_REMAT != 0;
 __device__ __forceinline__ uint32_t lane_id_fresh() {
@@ -267,6 +267,7 @@ __device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const Shar
     if (shaded) {
 #if defined(__HIPCC__)
         if constexpr (kUvRecompute) {   // (u, v) of the closest hit (rt_wavefront.h RT_UV_RECOMPUTE)
+            RT_CHECK(h.prim < sc.n_tris, 1, h.prim, h.prim = 0);
             const float4 *t = sc.tri + 3 * (size_t)h.prim;
             const float4 t0 = t[0], t1 = t[1], t2 = t[2];
             TriHit th;
