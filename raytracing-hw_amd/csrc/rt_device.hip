@@ -1844,6 +1844,8 @@ __global__ void __launch_bounds__(256) coop_check_kernel(const float4 *tri, int 
     bool active = valid;
     for (int it = 0; it < 64 && __any(active); ++it)   // (bounded: 7 triangles, 64 lanes, 8 per round)
         if (rtd::trav_step_coop<false, kLeaves, false>(sc, r, T, S, gn, cnt, active, round_min)) active = false;
+    // the step keeps (t, triangle) only: (u, v) as the shading pass recomputes them
+    if (rtd::kUvRecompute && valid && T.best.prim >= 0) rtd::hit_uv(sc, r, T.best);
     // sequential reference: trav_step's per-lane loop, one triangle at a time
     float acc = 1e9f;
     rtd::Hit best{1e9f, 0.f, 0.f, -1};

@@ -268,12 +268,7 @@ __device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const Shar
 #if defined(__HIPCC__)
         if constexpr (kUvRecompute) {   // (u, v) of the closest hit (rt_wavefront.h RT_UV_RECOMPUTE)
             RT_CHECK(h.prim < sc.n_tris, 1, h.prim, h.prim = 0);
-            const float4 *t = sc.tri + 3 * (size_t)h.prim;
-            const float4 t0 = t[0], t1 = t[1], t2 = t[2];
-            TriHit th;
-            tri_hit_bl(V3{t0.x, t0.y, t0.z}, V3{t0.w, t1.x, t1.y}, V3{t1.z, t1.w, t2.x}, L.r, th);
-            h.u = th.u;
-            h.v = th.v;
+            hit_uv(sc, L.r, h);
         }
 #endif
         Rng rng = lane_rng(L);

@@ -622,6 +622,17 @@ struct LdsStackT {
 #endif
 constexpr bool kUvRecompute = RT_UV_RECOMPUTE != 0;
 
+// (u, v) of a closest hit whose (t, triangle) the coop leaf step found (RT_UV_RECOMPUTE): the
+// same Moller-Trumbore test of the same triangle and ray, so the bits the step would have kept.
+__device__ __forceinline__ void hit_uv(const DevScene &sc, const Ray &r, Hit &h) {
+    const float4 *t = sc.tri + 3 * (size_t)h.prim;
+    const float4 t0 = t[0], t1 = t[1], t2 = t[2];
+    TriHit th;
+    tri_hit_bl(V3{t0.x, t0.y, t0.z}, V3{t0.w, t1.x, t1.y}, V3{t1.z, t1.w, t2.x}, r, th);
+    h.u = th.u;
+    h.v = th.v;
+}
+
 // One step of the quad reduction: take the partner lane's (t, u, v, index) when its t is
 // less, or equal with a lower index.
 template <int CTL>
