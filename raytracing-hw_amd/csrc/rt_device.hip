@@ -84,6 +84,11 @@ constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #define RT_PACK_TRAV 1
 #endif
 constexpr bool kPackTrav = RT_PACK_TRAV != 0;
+// ... in the runahead kernel too (A/B: it spills no VGPR at its 4 waves/SIMD)
+#ifndef RT_PACK_SPEC
+#define RT_PACK_SPEC 0
+#endif
+constexpr bool kPackSpec = RT_PACK_SPEC != 0;
 #ifndef RT_INV_RECOMPUTE
 #define RT_INV_RECOMPUTE 1
 #endif
@@ -542,7 +547,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 tbk.c[2] += (unsigned long long)__popcll(__ballot(L.state != rtd::M_IDLE));
 #endif
             } while (true);
-        } else if (kPackTrav && kInnerTrav && !LSPLIT && !kSpec && !FAST) {
+        } else if (kPackTrav && kInnerTrav && !LSPLIT && (!kSpec || kPackSpec) && !FAST) {
             // shading pass (the inner loop above runs every traversal iteration): a lane that
             // does not shade keeps its phase, stack depth and state packed in one register
             // through the pass (RT_PACK_TRAV)
@@ -553,7 +558,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             if (L.state == rtd::M_READY) {
                 L.T.phase = 0;   // dead in a READY lane (its stack is empty: T.sp == 0)
                 L.T.sp = 0;
-                rtd::mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, S, cnt);
+                rtd::mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, S, cnt, kSpec && tail);
             } else {
                 L.T.phase = (int)(pk & 3u);
                 L.state = (int)((pk >> 2) & 7u);
@@ -568,7 +573,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             // RT_UV_RECOMPUTE; frame -1.5% alone, -2.6% with it: profiles/r05k_ab.jsonl).  0: A/B.
             if (kInvRecompute && shade_now) L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
         }
-        if (kPackTrav && kInvRecompute && kInnerTrav && !LSPLIT && !kSpec && !FAST && shade_now)
+        if (kPackTrav && kInvRecompute && kInnerTrav && !LSPLIT && (!kSpec || kPackSpec) && !FAST && shade_now)
             L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
 #ifdef RT_MEGA_PROF
         {
