@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-5 call: the plain kernel's step knobs re-tuned on the packed build: leaf rounds while
+# >= 4 / 16 leaf lanes are unserved (8 now), 3 stack pops per step (2 now), shading at 52 READY
+# lanes (48 now); frame (and shards), two runs.
+set -o pipefail
+cd "$(dirname "$0")/.."
+V=raytracing-hw_amd
+REPS=2 SHARD_STEPS=1 bash tools/r05_ab.sh r05q_ab.jsonl default $V/v_rm4/librt_hw_amd.so $V/v_rm16/librt_hw_amd.so \
+  $V/v_pops3/librt_hw_amd.so $V/v_sh52/librt_hw_amd.so
+# the bench line again, now that profiles/ holds this build's counter passes (roofline.traffic, issue)
+timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 > gpurun_out/r05_bench2.json 2> gpurun_out/r05_bench2.err || { tail -5 gpurun_out/r05_bench2.err; exit 1; }
+tail -c 400 gpurun_out/r05_bench2.json
