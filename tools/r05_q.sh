@@ -10,3 +10,9 @@ REPS=2 SHARD_STEPS=1 bash tools/r05_ab.sh r05q_ab.jsonl default $V/v_rm4/librt_h
 # the bench line again, now that profiles/ holds this build's counter passes (roofline.traffic, issue)
 timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 > gpurun_out/r05_bench2.json 2> gpurun_out/r05_bench2.err || { tail -5 gpurun_out/r05_bench2.err; exit 1; }
 tail -c 400 gpurun_out/r05_bench2.json
+# the 2- and 4-way splits of the final build (all shards; slowest = the N-GPU frame)
+: > gpurun_out/r05q_splits.jsonl
+for w in 4 2; do
+  timeout -k 10 150 python3 tools/order_ab.py --natural 0 --full 0 --shard-steps 1 --world $w >> gpurun_out/r05q_splits.jsonl 2>>gpurun_out/r05q_splits.err || exit 1
+  tail -1 gpurun_out/r05q_splits.jsonl
+done
