@@ -417,3 +417,20 @@ def test_sponza_dragon_c5_pixels_vs_oracle(gpu, oracle, name, W, H):
     for p in pix:
         ref, _, _ = oracle.render(arrays, S, int(p), int(p) + 1, threads=1)
         assert np.array_equal(rtref.bits(out[p]), rtref.bits(ref[0])), f"pixel {p}"
+
+
+def test_idle_lanes_after_another_kernel(gpu):
+    """A lane-resident launch with fewer pixels than lanes right after a wavefront launch: the
+    lanes that never get a pixel start with the previous kernel's register contents, and the
+    shading pass packs their phase and stack depth with their state (rt_device.hip
+    RT_PACK_TRAV), so the kernel sets both at its start.  Counting and plain renders of the
+    33x17 frame (561 pixels, 768 lanes) after the wavefront kernel on 64x64 must be the
+    reference's sums (round 5: this sequence faulted before the fix)."""
+    big = gpu.Scene.from_view(rtref.ref_arrays(gpu, "cornell", 64, 64, 8))
+    _sums(big, 8, count=True, kernel=4)
+    small = gpu.Scene.from_view(rtref.ref_arrays(gpu, "cornell", 33, 17, 3))
+    ref = rtref.golden("cornell_sums_33x17x3.rtd")["sums"].reshape(-1, 3)
+    for kw in [dict(count=True, heavy_order=True), dict(count=True, natural_order=True), dict(runahead=False)]:
+        _sums(big, 8, count=True, kernel=4)
+        out, _ = _sums(small, 3, **kw)
+        assert (rtref.bits(out) == rtref.bits(ref)).all(), kw

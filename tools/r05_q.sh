@@ -16,3 +16,6 @@ for w in 4 2; do
   timeout -k 10 150 python3 tools/order_ab.py --natural 0 --full 0 --shard-steps 1 --world $w >> gpurun_out/r05q_splits.jsonl 2>>gpurun_out/r05q_splits.err || exit 1
   tail -1 gpurun_out/r05q_splits.jsonl
 done
+# the idle-lane regression test (the r05m / r05n fault sequence)
+timeout -k 10 200 python3 -u -m pytest tests/test_gpu_parity.py -k idle_lanes -x -v --timeout 120 --timeout-method thread > gpurun_out/r05q_idle_test.txt 2>&1 || { tail -20 gpurun_out/r05q_idle_test.txt; exit 1; }
+tail -2 gpurun_out/r05q_idle_test.txt
