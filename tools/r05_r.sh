@@ -1,6 +1,5 @@
 #!/bin/bash
 # Round-5 call: the GPU suite and smoke() on the exact final tree (after the last rebuild).
-# RT_TID_REMAT on, idle lanes' phase / stack depth set at kernel start).
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
