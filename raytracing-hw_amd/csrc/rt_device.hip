@@ -84,7 +84,8 @@ constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #define RT_PACK_TRAV 1
 #endif
 constexpr bool kPackTrav = RT_PACK_TRAV != 0;
-// ... in the runahead kernel too (A/B: it spills no VGPR at its 4 waves/SIMD)
+// ... in the runahead kernel too (A/B: that kernel spills no VGPR at its 4 waves/SIMD; 8-way
+// shards 183.5-185.0 vs 182.7-184.1 ms, at 5 waves/SIMD 200.5-201.5: profiles/r05p_ab.jsonl)
 #ifndef RT_PACK_SPEC
 #define RT_PACK_SPEC 0
 #endif
@@ -554,7 +555,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             // (phase < 4, state < 8 and sp <= kStack in every lane: all three are set at the
             // kernel's start and only ever assigned those values)
             uint32_t pk = (uint32_t)L.T.phase | (uint32_t)L.state << 2 | (uint32_t)L.T.sp << 5;
-            asm volatile("" : "+v"(pk));
+            asm volatile("" : "+v"(pk));   // (opaque: the compiler cannot fold the unpacking back)
             if (L.state == rtd::M_READY) {
                 L.T.phase = 0;   // dead in a READY lane (its stack is empty: T.sp == 0)
                 L.T.sp = 0;
