@@ -23,8 +23,12 @@ roofline = rank 0's render kernel.  Default (kernel 0, lane-resident rt_mega_ker
            With --kernel 4 (wavefront) it is the extend kernel alone: 24 B per AABB test +
            36 B per triangle test + 44 B of ray/hit I/O per ray, per launch / its average
            duration.  Peak: 8 TB/s HBM3E.  `traffic` is the HBM-side bytes per launch from
-           the committed rocprofv3 PMC passes of this command (2 x FETCH_SIZE + WRITE_SIZE,
-           the guide's gfx950 correction), `traffic_undoubled` without the doubling and
+           the committed rocprofv3 PMC passes of this command: FETCH_SIZE x the calibrated
+           factor of this kernel's load shapes + WRITE_SIZE.  The factor comes from
+           tools/fetch_calib.hip (profiles/<CALIB_PREFIX>_fetch_calib.csv: FETCH_SIZE against
+           the 128-B lines filled, per shape: 64-B node pairs, 48-B triangle quads, 4-B texel
+           gathers), weighted by the shapes' shares of the algorithmic bytes; `traffic_range`
+           spans the shapes' factors, `traffic_undoubled` is FETCH_SIZE as counted (+ WRITE_SIZE),
            `traffic_frac` = traffic / launch time / peak.
 cpu_baseline: the reference itself (oracle/_ref/ref_render, built from /root/reference's
            sources) timing its Scene::render loop on the host cores this process may use
@@ -39,6 +43,9 @@ roofline.bound follows the committed counters: "latency/issue" when the HBM-side
            "unmeasured" when no PMC pass of the command is committed.  --gpus N reads rank 0's
            shard passes (profiles/<SHARD_PROFILE_PREFIX>_shard_*_w<N>.csv, tools/pmc_shard.sh)
            for the kernel that rendered it (the runahead instantiation at 4 and 8 ways).
+ranks:    --gpus N: every rank's render kernel time, pre-pass time, schedule, rays and
+           algorithmic roofline fraction (all-gathered), and the slowest rank: the N-GPU step is
+           as slow as it.
 frame_matches_reference: the 8-bit frame's sha1 against the reference's own finished frame of
            the same workload (tests/golden/golden_meta.json "frames"), computed after the timed
            region.
@@ -63,6 +70,9 @@ PROFILE_PREFIX = "r05"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv 
 # profiles/<prefix>_shard_{fetch,write,sq1,sq2}_w<N>.csv: rank 0's shard of the N-way split
 # (tools/pmc_shard.sh), the counters of an --gpus N line
 SHARD_PROFILE_PREFIX = "r05"
+# profiles/<prefix>_fetch_calib.csv: FETCH_SIZE per filled 128-B line for each load shape
+# (tools/fetch_calib.sh)
+CALIB_PREFIX = "r06"
 # rocprofv3 names of the two parity instantiations of the default kernel: the plain one (one
 # GPU) and the runahead one (shards of at most 2 pixels per lane: the 4- and 8-way splits)
 KERNEL_PLAIN = "void rt_mega_kernel<false, false, false, false>"
@@ -202,13 +212,40 @@ def reference_frame_sha1(scene, W, H, S):
     return None
 
 
-def pmc_traffic(fetch_csv, write_csv, kname):
+def fetch_calibration(shares):
+    """FETCH_SIZE -> HBM bytes factor for the render kernel's loads: the committed calibration
+    (tools/fetch_calib.sh: per shape, lines x 128 B / FETCH_SIZE bytes on a 2 GiB buffer)
+    weighted by `shares` (the kernel's algorithmic bytes per shape: node pairs, triangles,
+    texels), and the shapes' min / max factors.  Without a committed calibration: the guide's
+    streaming factor 2 (uncalibrated for these shapes)."""
+    import csv
+    path = os.path.join(ROOT, "profiles", f"{CALIB_PREFIX}_fetch_calib.csv")
+    fac = {}
+    if os.path.exists(path):
+        for row in csv.DictReader(open(path)):
+            if row["hbm_per_fetch"] not in ("", "None"):
+                fac[row["kernel"]] = float(row["hbm_per_fetch"])
+    shapes = ["calib_pair", "calib_tri", "calib_texel"]
+    if not all(k in fac for k in shapes):
+        return 2.0, 2.0, 2.0, "uncalibrated: x2 (MI355X_MICROARCH.md streaming-read factor)"
+    tot = sum(shares) or 1.0
+    f = sum(fac[k] * w for k, w in zip(shapes, shares)) / tot
+    vals = [fac[k] for k in shapes]
+    return f, min(vals), max(vals), os.path.relpath(path, ROOT)
+
+
+def pmc_traffic(fetch_csv, write_csv, kname, shares):
     """HBM-side bytes per launch of kernel `kname` from rocprofv3 PMC summaries
     (tools/profile.sh, tools/pmc_shard.sh: separate --pmc passes of the same workload):
-    FETCH_SIZE doubled (the gfx950 correction of MI355X_MICROARCH.md, HBM section; FETCH_SIZE
-    counts half of the bytes of 16-B-per-lane reads) plus WRITE_SIZE, both KiB per dispatch."""
+    FETCH_SIZE x the calibrated factor (fetch_calibration) plus WRITE_SIZE, both KiB per
+    dispatch.  Returns (bytes, low, high, FETCH_SIZE + WRITE_SIZE as counted, calibration)."""
     f, w = pmc_mean(fetch_csv, "FETCH_SIZE", kname), pmc_mean(write_csv, "WRITE_SIZE", kname)
-    return None if f is None or w is None else (2.0 * f * 1024.0 + w * 1024.0, f * 1024.0 + w * 1024.0)
+    if f is None or w is None:
+        return None
+    fac, lo, hi, src = fetch_calibration(shares)
+    fb, wb = f * 1024.0, w * 1024.0
+    return fac * fb + wb, lo * fb + wb, hi * fb + wb, fb + wb, {"factor": round(fac, 4), "min": lo, "max": hi,
+                                                                "source": src}
 
 
 def main():
@@ -375,6 +412,23 @@ def main():
                      "note": "RT_FLAG_FAST: Philox4x32-10 seed per (pixel, sample), work units of `chunk` samples; "
                              "statistically equivalent to the reference, NOT bit-identical (not the headline)"}
 
+    def all_gather_rows(vals):
+        """Every rank's `vals` (a list of floats), in rank order."""
+        if world == 1:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        if share:
+            t = t.cpu()
+        outs = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return [o.tolist() for o in outs]
+
+    # every rank's own render: kernel time, pre-pass, schedule, rays, algorithmic bytes
+    my_bytes = (B_AABB * (counts["aabb_tests"] + counts["light_aabb_tests"])
+                + B_TRI * (counts["tri_tests"] + counts["light_tri_tests"]) + B_SHADE * counts["shading_hits"])
+    per_rank = all_gather_rows([float(np.mean(kernel_ms)), float(np.max(kernel_ms)), float(np.mean(order_ms)),
+                                float(sched), float(counts["rays"]), float(my_bytes)])
+
     keys = ["rays", "aabb_tests", "tri_tests", "light_queries", "light_aabb_tests", "light_tri_tests", "shading_hits"]
     local_counts = torch.tensor([counts[k] for k in keys], dtype=torch.float64, device="cuda")
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -404,7 +458,10 @@ def main():
             bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
             kname = KERNEL_SPEC if sched & rt.SCHED_RUNAHEAD else KERNEL_PLAIN
         achieved = bytes_launch / avg_s / 1e9
-        traffic, traffic_u, traffic_src, issue = None, None, None, None
+        traffic, traffic_u, traffic_src, issue, traffic_rng, calib = None, None, None, None, None, None
+        # the kernel's algorithmic bytes per load shape (node pairs, triangles, texels + shading)
+        shares = [B_AABB * (c0["aabb_tests"] + c0["light_aabb_tests"]), B_TRI * (c0["tri_tests"] + c0["light_tri_tests"]),
+                  B_SHADE * c0["shading_hits"]]
         if args.traffic_from != "none":
             prefix = args.traffic_from
             default_cfg = (args.scene, W, H, S, args.kernel) == ("sponza", 1920, 1080, 256, 0)
@@ -414,9 +471,11 @@ def main():
             if prefix:
                 fc, wc = pmc_file(prefix, "fetch", world), pmc_file(prefix, "write", world)
                 if os.path.exists(fc) and os.path.exists(wc):
-                    t = pmc_traffic(fc, wc, kname)
+                    t = pmc_traffic(fc, wc, kname, shares)
                     if t is not None:
-                        traffic, traffic_u = t[0] / launches, t[1] / launches
+                        traffic, traffic_u = t[0] / launches, t[3] / launches
+                        traffic_rng = [int(t[1] / launches), int(t[2] / launches)]
+                        calib = t[4]
                         traffic_src = os.path.relpath(fc, ROOT) + " + " + os.path.relpath(wc, ROOT)
                 issue = pmc_issue(prefix, kname, world)
         frac = achieved / HBM_PEAK_GBS
@@ -463,7 +522,9 @@ def main():
             "roofline": {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(frac, 4),
                          "traffic": None if traffic is None else int(traffic),
+                         "traffic_range": traffic_rng,
                          "traffic_undoubled": None if traffic_u is None else int(traffic_u),
+                         "fetch_calibration": calib,
                          "traffic_frac": None if traffic_frac is None else round(traffic_frac, 4),
                          "issue": issue,
                          "traffic_source": traffic_src,
@@ -479,6 +540,19 @@ def main():
                         "below 128 spp)"},
             "fast_mode": fast_line,
         }
+        sched_names = {rt.SCHED_LANE: "lane-resident", rt.SCHED_RUNAHEAD: "runahead", rt.SCHED_FAST: "fast",
+                       rt.SCHED_LIGHT_SPLIT: "light-split", rt.SCHED_WAVEFRONT: "wavefront"}
+        ranks = []
+        for r, (kms, kmax, oms, sc, rays_r, bytes_r) in enumerate(per_rank):
+            ranks.append({"rank": r, "render_ms": round(kms, 3), "render_ms_max": round(kmax, 3),
+                          "order_ms": round(oms, 3),
+                          "schedule": "+".join(v for b, v in sched_names.items() if int(sc) & b) or None,
+                          "rays": int(rays_r), "roofline_frac": round(bytes_r / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})
+        slow = max(ranks, key=lambda x: x["render_ms"])
+        line["ranks"] = ranks
+        line["slowest_rank"] = {"rank": slow["rank"], "render_ms": slow["render_ms"],
+                                "spread_ms": round(slow["render_ms"] - min(x["render_ms"] for x in ranks), 3),
+                                "gather_and_host_ms": round(elapsed / args.steps * 1e3 - slow["render_ms"], 3)}
         if world == 1 and not args.no_cpu_baseline:
             # the host cores this process may use: min(nproc, cgroup quota); --cpu-threads overrides
             quota = cpu_quota()

@@ -129,6 +129,10 @@ typedef struct {
  * runahead): same bits, shorter frame tail.  This flag turns it off.  (Counting renders,
  * count = 1, never use it: their counters are those of the sequential chain.) */
 #define RT_FLAG_NO_RUNAHEAD 16
+/* Every defined flag; a call with any other bit set fails with RT_ERR_ARG (e.g. ABI 5's
+ * RT_FLAG_POOL = 64, removed in ABI 6). */
+#define RT_FLAG_ALL (RT_FLAG_KERNEL_TIMES | RT_FLAG_FAST | RT_FLAG_LIGHT_SPLIT | RT_FLAG_NATURAL_ORDER | \
+                     RT_FLAG_NO_RUNAHEAD | RT_FLAG_HEAVY_ORDER)
 
 typedef struct {
     uint64_t pixels;        /* pixels rendered by this call                               */

@@ -106,6 +106,10 @@ ABI = {
 }
 
 _lib_handle = None
+# debug builds (make -C raytracing-hw_amd debug, RT_LIB=.../debug/librt_hw_amd.so) export
+# rt_debug_take: every render then raises on a recorded device check (rt_path.h RT_CHECK)
+# unless debug_raise is cleared (tests that provoke one)
+debug_raise = True
 
 
 def lib():
@@ -120,8 +124,40 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
+        if hasattr(h, "rt_debug_take"):
+            h.rt_debug_take.restype = ctypes.c_int
+            h.rt_debug_take.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+            h.rt_debug_set_poison.restype = ctypes.c_int
+            h.rt_debug_set_poison.argtypes = [ctypes.c_int]
         _lib_handle = h
     return _lib_handle
+
+
+def is_debug_build():
+    return hasattr(lib(), "rt_debug_take")
+
+
+def debug_take():
+    """Debug builds: the first device check violation since the last call (code << 56 | value),
+    0 = none; None on a release build."""
+    if not is_debug_build():
+        return None
+    w = ctypes.c_uint64(0)
+    _check(lib().rt_debug_take(ctypes.byref(w)))
+    return int(w.value)
+
+
+def debug_set_poison(on):
+    """Debug builds: poison every lane's traversal phase and stack depth at the lane-resident
+    kernel's start (the packing test)."""
+    _check(lib().rt_debug_set_poison(int(on)))
+
+
+def _after_render():
+    if debug_raise and _lib_handle is not None and hasattr(_lib_handle, "rt_debug_take"):
+        w = debug_take()
+        if w:
+            raise RtError(f"device check {w >> 56} failed (value {w & ((1 << 56) - 1):#x})")
 
 
 class RtError(RuntimeError):
@@ -180,6 +216,7 @@ class Scene:
         out_i = np.zeros((n, 6), np.int64)
         _check(lib().rt_intersect_rays(self._h, n, org.ctypes.data_as(_c_f), dirs.ctypes.data_as(_c_f),
                                        out_f.ctypes.data_as(_c_f), out_i.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        _after_render()
         return out_f, out_i
 
     def __del__(self):
@@ -239,6 +276,7 @@ class Scene:
                          light_split=light_split, natural_order=natural_order, runahead=runahead,
                          heavy_order=heavy_order)
         _check(lib().rt_render(self._h, ctypes.byref(p), out.ctypes.data_as(_c_f), ctypes.byref(st)))
+        _after_render()
         return out, st.as_dict()
 
     def render_multi(self, spp=None, n_devices=0, row_block=8, count=False, kernel=0, fast=False, fast_chunk=0):
@@ -248,6 +286,7 @@ class Scene:
         st = RtStats()
         p = self._params(spp, 0, 1, row_block, count, kernel, fast=fast, fast_chunk=fast_chunk)
         _check(lib().rt_render_multi(self._h, ctypes.byref(p), n_devices, out.ctypes.data_as(_c_f), ctypes.byref(st)))
+        _after_render()
         return out, st.as_dict()
 
     def render_frame(self, spp=None, n_shards=0, devices=None, row_block=8, sums=True, rgb=True, kernel=0,
@@ -270,6 +309,7 @@ class Scene:
                                      dev.ctypes.data_as(_c_i) if dev is not None else None,
                                      out_rgb.ctypes.data_as(_c_b) if rgb else None,
                                      out_sum.ctypes.data_as(_c_f) if sums else None, ctypes.byref(st)))
+        _after_render()
         return out_rgb, out_sum, st.as_dict()
 
     def render_device(self, d_out_ptr, stream_ptr=None, spp=None, rank=0, world=1, row_block=8, count=False,
@@ -283,6 +323,7 @@ class Scene:
         st = RtStats() if stats else None
         _check(lib().rt_render_device(self._h, ctypes.byref(p), ctypes.c_void_p(d_out_ptr),
                                       ctypes.c_void_p(stream_ptr or 0), ctypes.byref(st) if st else None))
+        _after_render()
         return st.as_dict() if st else None
 
     def render(self):

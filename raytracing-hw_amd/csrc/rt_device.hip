@@ -68,13 +68,6 @@ constexpr int kMegaWpeSpec = RT_SPEC_WPE;
 #endif
 constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
-// Traversal iterations between two shading passes run as an inner loop of their own (no pixel
-// claim, runahead pass or schedule decision per iteration).  0: one iteration per pass of the
-// main loop (round 2), for A/B builds.
-#ifndef RT_INNER_TRAV
-#define RT_INNER_TRAV 1
-#endif
-constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 // RT_PACK_TRAV: through a shading pass, a lane that does not shade holds its traversal phase,
 // stack depth and state packed in one register (the loop body below).  With RT_TID_REMAT
 // (rt_mega.h) the plain kernel spills 16 VGPRs instead of 33 and writes 0.11 instead of
@@ -84,28 +77,15 @@ constexpr bool kInnerTrav = RT_INNER_TRAV != 0;
 #define RT_PACK_TRAV 1
 #endif
 constexpr bool kPackTrav = RT_PACK_TRAV != 0;
-// ... in the runahead kernel too (A/B: that kernel spills no VGPR at its 4 waves/SIMD; 8-way
-// shards 183.5-185.0 vs 182.7-184.1 ms, at 5 waves/SIMD 200.5-201.5: profiles/r05p_ab.jsonl)
-#ifndef RT_PACK_SPEC
-#define RT_PACK_SPEC 0
-#endif
-constexpr bool kPackSpec = RT_PACK_SPEC != 0;
 #ifndef RT_INV_RECOMPUTE
 #define RT_INV_RECOMPUTE 1
 #endif
 constexpr bool kInvRecompute = RT_INV_RECOMPUTE != 0;
-// The lane-resident kernel's traversal state shares the node and leaf fields (rt_wavefront.h
-// TravStateU; the runahead kernel keeps TravState).  0: TravState everywhere, for A/B builds.
-#ifndef RT_PLAIN_TRAV_SHARED
-#define RT_PLAIN_TRAV_SHARED 1
-#endif
-constexpr bool kPlainTravShared = RT_PLAIN_TRAV_SHARED != 0;
-// ... whose leaf work is spread over the wave (rt_wavefront.h trav_step_coop).  0: per-lane
-// leaf steps of RT_LEAF_N triangles, for A/B builds.
-#ifndef RT_COOP_LEAF
-#define RT_COOP_LEAF 1
-#endif
-constexpr bool kCoopLeaf = RT_COOP_LEAF != 0;
+// Traversal iterations between two shading passes run as an inner loop of their own (no pixel
+// claim, runahead pass or schedule decision per iteration), one cooperative step each
+// (rt_wavefront.h trav_step_coop: leaf work spread over the wave).  The lane-resident
+// kernel's traversal state shares the node and leaf fields (rt_wavefront.h TravStateU; the
+// runahead kernel keeps TravState).
 // Leaf lanes a coop step serves (32 B of LDS per wave each).  The plain kernel's block is at
 // 30 KB and must stay within 32 KB minus what the runtime keeps, for 5 blocks per CU: 16
 // records (32 KB) measured 1426 ms against 1272 at 8 (4 blocks per CU).  The runahead kernel
@@ -152,12 +132,6 @@ constexpr int kCoopRoundNodes = 4096;
 #ifndef RT_ORDER_RADIUS
 #define RT_ORDER_RADIUS 4
 #endif
-#ifndef RT_ORDER_SNAKE
-#define RT_ORDER_SNAKE 0
-#endif
-#ifndef RT_ORDER_NOSPREAD
-#define RT_ORDER_NOSPREAD 0
-#endif
 constexpr int kOrderSpp = RT_ORDER_SPP;       // samples per pixel of the counting pre-pass
 constexpr int kOrderRadius = RT_ORDER_RADIUS;  // box filter of the pre-pass costs ((2r+1)^2 pixels)
 // The pre-pass and sort cost about one sample per pixel, so below kOrderMinSpp the order
@@ -174,6 +148,13 @@ constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units 
 #define RT_SPEC_PIXELS_PER_LANE 2
 #endif
 constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
+// Runahead kernel, shards of at most one pixel per resident lane: the whole resident grid with
+// a static share of the pixels per wave (rt_mega_kernel static_per), instead of one lane per
+// pixel over ceil(pixels / 256) blocks.
+#ifndef RT_SPEC_STATIC
+#define RT_SPEC_STATIC 0
+#endif
+constexpr bool kSpecStatic = RT_SPEC_STATIC != 0;
 // Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
 // holds at most 64 / k pixels and the grid grows k-fold (lockstep study).
 #ifndef RT_CLAIM_STRIDE
@@ -188,8 +169,6 @@ constexpr double kWfCompactBelow = 0.75;   // wavefront: dense queue until this 
 struct rt_device_blob {
     std::vector<uint8_t> bytes;
     size_t o_tri, o_attr, o_tan, o_node, o_light, o_lnode, o_mf, o_mt, o_nt, o_ti, o_tx, o_lut;
-    size_t o_node_soa = 0, o_tri_soa = 0;   // RT_SOA builds only
-    long long node_plane = 0, tri_plane = 0;
 };
 
 struct rt_device_scene {
@@ -353,10 +332,13 @@ struct TbAcc {
 // SPEC (parity renders without counting): a wave whose claim finds the queue empty enters its
 // tail and runs speculative sample runahead (rt_mega.h spec_manage) on its idle lanes.  A
 // separate instantiation, so the kernel without it keeps its own register allocation.
+// `static_per` > 0 (SPEC, shards of at most one pixel per resident lane): no queue; wave w of
+// the grid takes queue items [w * static_per, (w + 1) * static_per), its lanes below static_per
+// one each, and enters its tail at once, so the lanes above run runahead jobs from the start.
 template <bool COUNT, bool FAST = false, bool LSPLIT = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPEC ? kMegaWpeSpec : kMegaWpe, 8)))
 rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
-               unsigned long long *queue, const int *order, unsigned *cost, int cs) {
+               unsigned long long *queue, const int *order, unsigned *cost, int cs, int static_per) {
     constexpr bool kSpec = SPEC && !COUNT && !FAST && !LSPLIT;
     const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels;
     const int lane = threadIdx.x & 63;
@@ -364,12 +346,6 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     // linear decode is computed: rt_path.h texel_decode)
     __shared__ float lut[256];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) lut[k] = sc_in.lut[k];
-    if constexpr (kSpec && rtd::kSpecShare) {   // the block's offer board (rt_mega.h RT_SPEC_SHARE)
-        for (int k = threadIdx.x; k < rtd::kOffers * rtd::kOfWords; k += blockDim.x) rtd::spec_board()[k] = 0u;
-        if (threadIdx.x == 0) rtd::spec_block_active()[0] = 0;
-        if (threadIdx.x < 4) rtd::spec_fdone()[threadIdx.x] = 0;
-        if (threadIdx.x < 4) rtd::spec_wave_active_lds[threadIdx.x] = 0;
-    }
     __syncthreads();
     DevScene sc = sc_in;
     sc.lut = lut;
@@ -381,7 +357,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     const rtd::NodeRec root = rtd::load_node(sc.node, 0);
     // lane state: the runahead kernel keeps TravState, the others share the node / leaf fields
     // (rt_wavefront.h TravStateU)
-    std::conditional_t<kSpec || !kPlainTravShared, rtd::MegaLane, rtd::MegaLaneU> L;
+    std::conditional_t<kSpec, rtd::MegaLane, rtd::MegaLaneU> L;
     L.pix = -1;
     L.state = rtd::M_IDLE;
     // A lane that never gets a pixel still takes part in the shading pass's packing
@@ -390,10 +366,18 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     // turn an idle lane's state into TRAV or READY).
     L.T.phase = rtd::TP_POP;
     L.T.sp = 0;
+#if defined(RT_DEBUG_CHECKS)
+    // debug builds: rt_debug_set_poison(1) leaves out-of-range leftovers in every lane's phase
+    // and stack depth instead (the state round 5's fault came from), to show that the packing
+    // below masks them and that its check reports them (tests/test_gpu_parity.py)
+    if (rt_debug_poison) {
+        L.T.phase = 0x7ffffffd;
+        L.T.sp = 0x3ffffff;
+    }
+#endif
     L.wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x) & ~63u;
     bool exhausted = false;
     bool tail = false, wave_room = false;
-    unsigned idle_checks = 0;   // RT_SPEC_SHARE helpers (below)
 #ifdef RT_MEGA_PROF
     unsigned long long pf[7] = {0, 0, 0, 0, 0, 0, 0};
     if (threadIdx.x < 8) rt_prof_lds[threadIdx.x] = 0;
@@ -404,6 +388,11 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     const unsigned long long wt0 = wall_clock64();
     TbAcc tbk;
 #endif
+    if (kSpec && static_per > 0) {
+        const long long p = (rtd::mega_slot() >> 6) * static_per + lane;
+        if (lane < static_per && p < n_items) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
+        exhausted = true;
+    }
     for (;;) {
         if (!exhausted) {   // lanes without work take the next items (one atomic per wave)
             const bool need = L.pix < 0 && (kClaimStride == 1 || lane % kClaimStride == 0);
@@ -429,7 +418,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         if constexpr (kSpec) {
             if (exhausted && !tail) {
                 if (lane == 0) rtd::spec_hint_take();
-                rtd::spec_convert(L, rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, lane);
+                rtd::spec_convert(L, sc, g, rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, lane);
                 tail = true;
                 wave_room = false;
 #ifdef RT_MEGA_PROF
@@ -438,14 +427,9 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             }
             if (tail) {
                 wave_room |= rtd::spec_hint_take();
-                bool share_pass = false;   // RT_SPEC_SHARE: an offer of ours is done, or one to take
-                if constexpr (rtd::kSpecShare)
-                    share_pass = rtd::spec_fdone_take() || (__any(L.state == rtd::M_IDLE) && rtd::spec_foreign_open());
-                if (__any(L.state == rtd::M_DONE_NEW) || share_pass || (wave_room && __any(L.state == rtd::M_IDLE))) {
+                if (__any(L.state == rtd::M_DONE_NEW) || (wave_room && __any(L.state == rtd::M_IDLE))) {
 #ifdef RT_MEGA_PROF
                     const long long c0 = clock64();
-#endif
-#ifdef RT_MEGA_PROF
                     tbk.c[5] += 1;
 #endif
                     wave_room = rtd::spec_manage(rtd::SpecLanes{L}, sc, g,
@@ -458,38 +442,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                     }
 #endif
                 }
-                if (!__any(L.state != rtd::M_IDLE)) {
-                    // RT_SPEC_SHARE: a wave with nothing left stays as a helper while the block
-                    // has unfinished pixels (their offers may come).  A wave whose own records
-                    // are unfinished (all its jobs on the board) always stays; a helper leaves
-                    // after 2^16 idle checks (about 10 ms) without work, so a bug cannot keep a
-                    // launch resident.
-                    if (!rtd::kSpecShare || rtd::block_active() == 0) break;
-                    if (rtd::wave_active() == 0 && ++idle_checks > (1u << 16)) break;
-#ifdef RT_SHARE_DEBUG
-                    // (diagnostics build: a wave idle this long with its own records unfinished is
-                    // stalled; report its records and the board once, then leave)
-                    if (rtd::wave_active() > 0 && ++idle_checks > (1u << 20)) {
-                        const rtd::SpecView V{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane};
-                        const uint4 a = *V.w(0, lane), b = *V.w(1, lane), c = *V.w(2, lane), d = *V.w(3, lane);
-                        if (lane == 0) {
-                            printf("[share stall] block %d wave %d wave_active %d block_active %d board:", (int)blockIdx.x,
-                                   (int)(threadIdx.x >> 6), rtd::wave_active(), rtd::block_active());
-                            for (int k = 0; k < rtd::kOffers; ++k)
-                                printf(" %x/%u/%u", rtd::spec_board()[k * rtd::kOfWords], rtd::spec_board()[k * rtd::kOfWords + 1],
-                                       rtd::spec_board()[k * rtd::kOfWords + 2]);
-                            printf("\n");
-                        }
-                        if (b.w & rtd::kRecActive)
-                            printf("[share stall]  block %d wave %d rec %d: f %u n %u epoch %u meta %x tab %08x%08x\n",
-                                   (int)blockIdx.x, (int)(threadIdx.x >> 6), lane, a.y, a.z, a.w, b.w, d.w, c.w);
-                        break;
-                    }
-#endif
-                    __builtin_amdgcn_s_sleep(4);
-                    continue;
-                }
-                idle_checks = 0;
+                if (!__any(L.state != rtd::M_IDLE)) break;
             } else if (!__any(L.pix >= 0)) {
                 break;
             }
@@ -522,21 +475,16 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             }
         }
 #endif
-        if (kInnerTrav && !LSPLIT && !shade_now) {
+        if (!LSPLIT && !shade_now) {
             // Traversal iterations until the wave would shade (the condition above): nothing
             // but trav_step and two ballots per iteration.  In a traversal iteration no lane
             // ends a path, so no lane claims a pixel and a tail wave's runahead records do not
             // change: the outer loop's work between two shading passes is only this.
             int kt = nt;
             do {
-                if (kCoopLeaf) {
-                    if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain, kSpec && kSpecMaskLoad>(
-                            sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV,
-                            kSpec ? st.round_min : kCoopRoundMinPlain))
-                        L.state = rtd::M_READY;
-                } else if (L.state == rtd::M_TRAV && rtd::trav_step<COUNT>(sc, L.r, L.T, S, nodes, cnt)) {
+                if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain, kSpec && kSpecMaskLoad>(
+                        sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV, kSpec ? st.round_min : kCoopRoundMinPlain))
                     L.state = rtd::M_READY;
-                }
                 const unsigned long long rb = __ballot(L.state == rtd::M_READY), tb = __ballot(L.state == rtd::M_TRAV);
                 kt = __popcll(tb);
                 if (kt == 0 || __popcll(rb) >= (kSpec ? kSpecShadeMin : kShadeMin)) break;
@@ -548,13 +496,16 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
                 tbk.c[2] += (unsigned long long)__popcll(__ballot(L.state != rtd::M_IDLE));
 #endif
             } while (true);
-        } else if (kPackTrav && kInnerTrav && !LSPLIT && (!kSpec || kPackSpec) && !FAST) {
+        } else if (kPackTrav && !LSPLIT && !kSpec && !FAST) {
             // shading pass (the inner loop above runs every traversal iteration): a lane that
             // does not shade keeps its phase, stack depth and state packed in one register
-            // through the pass (RT_PACK_TRAV)
-            // (phase < 4, state < 8 and sp <= kStack in every lane: all three are set at the
-            // kernel's start and only ever assigned those values)
-            uint32_t pk = (uint32_t)L.T.phase | (uint32_t)L.state << 2 | (uint32_t)L.T.sp << 5;
+            // through the pass (RT_PACK_TRAV).  phase < 4, state < 8 and sp <= kStack hold in
+            // every lane (set at the kernel's start, only ever assigned such values; checked in
+            // the debug build), and the fields are masked anyway, so that a stray bit of one
+            // can never reach another (round 5: an idle lane's leftover phase bit made it READY)
+            RT_CHECK((unsigned)L.T.phase < 4u && (unsigned)L.state < 8u && (unsigned)L.T.sp <= (unsigned)rtd::kStack, 14,
+                     (unsigned)L.T.phase | (unsigned long long)(unsigned)L.state << 32, (void)0);
+            uint32_t pk = ((uint32_t)L.T.phase & 3u) | ((uint32_t)L.state & 7u) << 2 | ((uint32_t)L.T.sp & 127u) << 5;
             asm volatile("" : "+v"(pk));   // (opaque: the compiler cannot fold the unpacking back)
             if (L.state == rtd::M_READY) {
                 L.T.phase = 0;   // dead in a READY lane (its stack is empty: T.sp == 0)
@@ -574,7 +525,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             // RT_UV_RECOMPUTE; frame -1.5% alone, -2.6% with it: profiles/r05k_ab.jsonl).  0: A/B.
             if (kInvRecompute && shade_now) L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
         }
-        if (kPackTrav && kInvRecompute && kInnerTrav && !LSPLIT && (!kSpec || kPackSpec) && !FAST && shade_now)
+        if (kPackTrav && kInvRecompute && !LSPLIT && !kSpec && !FAST && shade_now)
             L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
 #ifdef RT_MEGA_PROF
         {
@@ -650,16 +601,7 @@ __global__ void __launch_bounds__(256) rt_order_spread_kernel(const int *sorted,
     long long r = q;
     if (q < m) {
         const long long gi = q / per, j = q % per, a = m / per, b = m % per;
-#if RT_ORDER_NOSPREAD
-        r = q;   // (A/B: heaviest first, no spread: a wave's pixels are of one cost stratum)
-#elif RT_ORDER_SNAKE
-        // (A/B: odd strata dealt in reverse, so the wave holding a stratum's heaviest pixel
-        // gets the next stratum's lightest)
-        const long long size = a + (j < b ? 1 : 0);
-        r = j * a + (j < b ? j : b) + ((j & 1) ? size - 1 - gi : gi);
-#else
         r = j * a + (j < b ? j : b) + gi;
-#endif
     }
     order[q] = sorted[r];
 }
@@ -903,24 +845,6 @@ int ensure_blob(rt_scene *s) {
     std::vector<float> lut(512);
     rtd::fill_decode_lut(lut.data());
     b->o_lut = append(blob, lut);
-#if RT_SOA
-    {   // SoA planes of the BFS nodes and of the triangles (the coop traversal step reads these)
-        const std::vector<float> bn = rtd::bfs_nodes(s->node);
-        const size_t nn = bn.size() / 8, nt = s->tri.size() / 12;
-        const long long np = (long long)((nn + 3) & ~size_t(1)), tp = (long long)nt;
-        std::vector<float> ns((size_t)np * 2 * 4, 0.f), ts((size_t)std::max<long long>(tp, 1) * 3 * 4, 0.f);
-        for (size_t k = 0; k < nn; ++k) {
-            std::memcpy(&ns[4 * (1 + k)], &bn[8 * k], 4 * sizeof(float));
-            std::memcpy(&ns[4 * ((size_t)np + 1 + k)], &bn[8 * k + 4], 4 * sizeof(float));
-        }
-        for (size_t k = 0; k < nt; ++k)
-            for (int pl = 0; pl < 3; ++pl) std::memcpy(&ts[4 * ((size_t)pl * tp + k)], &s->tri[12 * k + 4 * pl], 4 * sizeof(float));
-        b->o_node_soa = append(blob, ns);
-        b->o_tri_soa = append(blob, ts);
-        b->node_plane = np;
-        b->tri_plane = tp;
-    }
-#endif
     blob.resize(((blob.size() + 255) & ~size_t(255)) + 256);
     s->blob = b;
     return RT_OK;
@@ -992,10 +916,6 @@ int ensure_device_scene(rt_scene *s, int device) {
     ds.tex_info = (const uint4 *)(base + b.o_ti);
     ds.texels = (const uint32_t *)(base + b.o_tx);
     ds.lut = (const float *)(base + b.o_lut);
-    ds.node_soa = b.o_node_soa ? (const float4 *)(base + b.o_node_soa) : nullptr;
-    ds.tri_soa = b.o_tri_soa ? (const float4 *)(base + b.o_tri_soa) : nullptr;
-    ds.node_plane = b.node_plane;
-    ds.tri_plane = b.tri_plane;
     ds.n_lights = (int)(s->light.size() / 16);
     ds.n_tris = (int)(s->tri.size() / 12);
     ds.n_nodes = (int)(s->node.size() / 8);
@@ -1172,7 +1092,7 @@ int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, lon
     w.n = n;
     w.lanes = (long long)blocks * 256;
     hipLaunchKernelGGL(pre, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, kOrderSpp, d->fast_part,
-                       d->counters + 8, d->queue + 1, (const int *)nullptr, cost, kOrderSpp);
+                       d->counters + 8, d->queue + 1, (const int *)nullptr, cost, kOrderSpp, 0);
     HIP_TRY(hipGetLastError());
     const unsigned nb = (unsigned)((n + 255) / 256);
     if (kOrderRadius > 0) {   // box-filtered costs: the pixel's neighbourhood estimates its expected work
@@ -1193,8 +1113,16 @@ int launch_order(rt_device_scene *d, const ShardGeom &g, hipStream_t stream, lon
     return RT_OK;
 }
 
+// Flag bits outside RT_FLAG_ALL (e.g. ABI 5's RT_FLAG_POOL) are an error, not ignored.
+int check_flags(const rt_params *p, const char *who) {
+    if (p->flags & ~RT_FLAG_ALL)
+        return rt_fail(RT_ERR_ARG, std::string(who) + ": unknown flag bits " + std::to_string(p->flags & ~RT_FLAG_ALL));
+    return RT_OK;
+}
+
 int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt_stats *st) {
     if (!s || !p || !d_out) return rt_fail(RT_ERR_ARG, "rt_render: NULL argument");
+    if (int rc = check_flags(p, "rt_render")) return rc;
     if (p->device < 0 || p->device >= kRtMaxDevices || !s->dev[p->device])
         return rt_fail(RT_ERR_ARG, "rt_render: scene not uploaded to device " + std::to_string(p->device));
     const int world = p->world > 0 ? p->world : 1, rank = p->rank, rb = p->row_block > 0 ? p->row_block : 8;
@@ -1259,7 +1187,14 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                                     : count ? rt_mega_kernel<true>
                                             : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
             sched = fast ? RT_SCHED_FAST : lsplit ? RT_SCHED_LIGHT_SPLIT : spec ? RT_SCHED_RUNAHEAD : RT_SCHED_LANE;
-            const unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
+            unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
+            // a shard of at most one pixel per resident lane: the whole resident grid, every wave
+            // with its share of the pixels at once (RT_SPEC_STATIC)
+            int static_per = 0;
+            if (spec && kSpecStatic && kClaimStride == 1 && n_items <= full_blocks * 256) {
+                blocks = (unsigned)full_blocks;
+                static_per = (int)((n_items + 4 * full_blocks - 1) / (4 * full_blocks));
+            }
             const long long slots = (long long)blocks * 256;   // lane slots
             // vertex records are addressed with 32-bit byte offsets (rt_path.h LaneRec)
             if ((unsigned long long)slots * (unsigned long long)s->ray_depth * 32ull >= (1ull << 32))
@@ -1274,7 +1209,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
                 // the spread deals one pixel of every cost stratum to each claim of 64 of the
                 // launch's first round (one per wave)
-                rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
+                rc = launch_order(d, g, stream, 4LL * blocks, static_per > 0 ? static_per : 64, &order);
                 if (rc) return rc;
                 ordered = true;
             }
@@ -1296,7 +1231,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
-                               (const int *)order, (unsigned *)nullptr, cs);
+                               (const int *)order, (unsigned *)nullptr, cs, static_per);
             HIP_TRY(hipGetLastError());
             if (fast) {
                 const long long n3 = g.n_pixels * 3;
@@ -1371,9 +1306,6 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                              "cycles in passes/wave=%.3g frontier jobs=%llu runahead jobs=%llu added=%llu "
                              "runahead jobs proven=%llu invalidations=%llu\n", sp[7], sp[7] ? (double)sp[0] / sp[7] : 0.0,
                              sp[0] ? (double)sp[1] / sp[0] : 0.0, (double)sp[1] / pf[7], sp[2], sp[3], sp[4], sp[5], sp[6]);
-                std::fprintf(stderr, "[mega prof] shared runahead: offers posted=%llu taken=%llu run to the end=%llu "
-                             "added (proven)=%llu reclaimed untaken=%llu cancelled=%llu\n", sp[8], sp[11], sp[9], sp[10],
-                             sp[12], sp[13]);
                 std::fprintf(stderr, "[mega prof] runahead chains: proven share of runahead jobs=%.3f, pixels completed "
                              "in the tail=%llu, mean time per chain link (completion / spp)=%.1f us\n",
                              sp[3] ? (double)sp[5] / (double)sp[3] : 0.0, sp[15], sp[15] ? (double)sp[14] / sp[15] / 100.0 : 0.0);
@@ -1505,6 +1437,7 @@ int rt_tonemap_u8_device(const float *d_sum, int32_t width, int32_t height, int3
 
 int rt_render(rt_scene *s, const rt_params *p, float *out, rt_stats *st) {
     if (!s || !p || !out) return rt_fail(RT_ERR_ARG, "rt_render: NULL argument");
+    if (int rc = check_flags(p, "rt_render")) return rc;
     return render_host(s, p, out, st);
 }
 
@@ -1523,6 +1456,7 @@ int rt_render(rt_scene *s, const rt_params *p, float *out, rt_stats *st) {
 int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int32_t *devices, uint8_t *out_rgb,
                     float *out_sum, rt_stats *st) {
     if (!s || !p || (!out_rgb && !out_sum)) return rt_fail(RT_ERR_ARG, "rt_render_frame: NULL argument");
+    if (int rc = check_flags(p, "rt_render_frame")) return rc;
     // (a devices array needs its length: one entry per shard, so n_shards must be given)
     if (devices && n_shards <= 0)
         return rt_fail(RT_ERR_ARG, "rt_render_frame: devices given without n_shards (one device per shard)");
@@ -1600,8 +1534,8 @@ int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int
     // rendered (launch waits for it: stats) and finished to 8 bits on the render stream; the
     // copy stream waits for that finish and copies the shard to the root's staging buffer,
     // while the render stream goes on with the next shard in the other buffer (it waits for
-    // that buffer's previous copy first).  The device's last copy is marked by fr_last, which
-    // the root's assembly waits for on the device, not on the host.
+    // that buffer's previous copy first).  The device's last copy is marked by fr_last: the
+    // root waits for its own on its stream, and for every peer's on the host (below).
     auto work = [&](size_t ui) {
         const int dev = uniq[ui];
         rt_device_scene *dd = s->dev[dev];
@@ -1720,6 +1654,7 @@ int rt_render_frame(rt_scene *s, const rt_params *p, int32_t n_shards, const int
 // The float frame over devices 0 .. n-1 (ABI 3 entry; rt_render_frame with shard r on device r).
 int rt_render_multi(rt_scene *s, const rt_params *p, int32_t n_devices, float *out, rt_stats *st) {
     if (!s || !p || !out) return rt_fail(RT_ERR_ARG, "rt_render_multi: NULL argument");
+    if (int rc = check_flags(p, "rt_render_multi")) return rc;
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     const int n = n_devices > 0 ? n_devices : ndev;
@@ -1764,8 +1699,15 @@ int rt_intersect_rays(rt_scene *s, int64_t n, const float *org, const float *dir
 // debug builds only: first recorded index violation (code << 56 | value), 0 = none
 int rt_debug_take(unsigned long long *word) {
     unsigned long long z = 0;
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(word, HIP_SYMBOL(rt_debug_word), sizeof z));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rt_debug_word), &z, sizeof z));
+    return RT_OK;
+}
+// debug builds only: poison every lane's traversal phase and stack depth at the lane-resident
+// kernel's start (rt_mega_kernel), for the packing test
+int rt_debug_set_poison(int on) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rt_debug_poison), &on, sizeof on));
     return RT_OK;
 }
 #endif

@@ -37,6 +37,7 @@ __device__ __forceinline__ const float4 *mega_nodes(const DevScene &sc) { return
 // M_DONE_NEW / M_DONE: a runahead job whose sample has ended, holding its colour and end
 // state until its pixel's frontier reaches it (speculative runahead, below).
 enum MegaState : int { M_IDLE = 0, M_TRAV = 1, M_READY = 2, M_LTRAV = 3, M_LREADY = 4, M_DONE_NEW = 5, M_DONE = 6 };
+static_assert(M_DONE < 8, "rt_mega_kernel packs a lane's state in 3 bits (RT_PACK_TRAV)");
 
 template <class TS>
 struct MegaLaneT {
@@ -188,7 +189,16 @@ __device__ __forceinline__ void mega_sample(ML &L, const DevScene &sc, const Sha
     mega_begin<COUNT>(L, root, cnt);
 }
 
-// A new pixel: seed its RNG (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1), first sample.
+// The RNG state shard pixel p's sample 0 starts from: minstd_rand seeded with the pixel
+// index (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1).
+__device__ __forceinline__ Rng pixel_seed(const DevScene &sc, const ShardGeom &g, int p) {
+    int px, py;
+    shard_xy(g, p, px, py);
+    const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
+    return Rng{seed == 0 ? 1u : seed, 0u, 0.f};
+}
+
+// A new pixel: seed its RNG, first sample.
 template <bool COUNT, class ML>
 __device__ __forceinline__ void mega_assign(ML &L, const DevScene &sc, const ShardGeom &g, int p,
                                             const NodeRec &root, Counters &cnt) {
@@ -196,10 +206,7 @@ __device__ __forceinline__ void mega_assign(ML &L, const DevScene &sc, const Sha
     lane_ctr_set(L, LaneCtr{0, 0, 0});
     lane_sum_set(L, V3{0.f, 0.f, 0.f});
     L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
-    int px, py;
-    shard_xy(g, p, px, py);
-    const uint32_t seed = (uint32_t)(py * sc.width + px) % 2147483647u;
-    lane_rng_set(L, Rng{seed == 0 ? 1u : seed, 0u, 0.f});
+    lane_rng_set(L, pixel_seed(sc, g, p));
     mega_sample<COUNT>(L, sc, g, root, cnt);
 }
 
@@ -496,9 +503,8 @@ __device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevSce
 // Diagnostics build (RT_MEGA_PROF): runahead event counts, printed by the launch.
 // [0] management passes [1] their cycles (per wave) [2] frontier jobs issued [3] runahead jobs
 // issued [4] jobs added [5] of them runahead jobs [6] invalidations [7] waves that reached a tail
-// (RT_SPEC_SHARE) [8] offers posted [9] offers run to the end by another wave [10] of them added
-// (proven) [11] offers taken [12] frontier offers reclaimed untaken [13] offers cancelled
-// [14] chain-link time sum (pixel completion since its wave's start / spp) [15] pixels completed
+// [8]-[13] unused [14] chain-link time sum (pixel completion since its wave's start / spp)
+// [15] pixels completed
 #if defined(RT_MEGA_PROF) && defined(__HIPCC__)
 // (per-block LDS sums, added to g_spec_prof once at the end of the kernel: global atomics on
 // eight words from every wave serialised the runahead kernel)
@@ -520,8 +526,8 @@ inline unsigned long long g_spec_prof[16];   // host test harness
 #define RT_SPEC_CHAIN_END(spp) do { } while (0)
 #endif
 
-// Record meta (plane 1 .w): bit 0 active, bit 1 X_f known (false until the wave's first job of
-// the pixel ends).  Window and issue rate, slowest 8-way shard of the headline frame: with
+// Record meta (plane 1 .w): bit 0 active, bit 1 X_f known (for a pixel that entered the tail
+// past its sample 0: false until the wave's first job of the pixel ends).  Window and issue rate, slowest 8-way shard of the headline frame: with
 // the round-3 traversal (inner loop, coop leaves, pop cap) window 3 with both runahead jobs
 // issued in one pass 208 ms; window 4 one job per pass 218, two 213, three 211; window 2
 // 212-215; window 6 228 (profiles/r03_ab.jsonl r03ad-af).  Fewer speculative jobs in flight
@@ -546,108 +552,16 @@ constexpr int kSpecWindow = RT_SPEC_WINDOW;   // jobs in flight per pixel at mos
 #endif
 constexpr bool kSpecLazy = RT_SPEC_LAZY != 0;   // spec_job_end: only frontier ends trigger a pass
 constexpr int kSpecIssue = RT_SPEC_ISSUE;     // runahead jobs a pixel gets per management pass
-// Block-shared runahead (RT_SPEC_SHARE, the cross-wave job table): a wave whose unfinished
-// pixels are few (at most kShareRecords records) posts jobs beyond its own window as OFFERS on
-// a board in the block's LDS, and any other wave of the block with idle lanes takes them: the
-// job runs in that wave, among its lanes, not in lockstep with the pixel's frontier.  The
-// result (colour, end state) goes back to the offer and the owner adds it exactly as a local
-// job's, only once the frontier reaches it with the start state proven (same bits).  A wave
-// whose own pixels are done stays resident as a helper while the block has unfinished pixels.
-#ifndef RT_SPEC_SHARE
-#define RT_SPEC_SHARE 0
-#endif
-#ifndef RT_SHARE_RECORDS
-#define RT_SHARE_RECORDS 16
-#endif
-#ifndef RT_SHARE_WINDOW
-#define RT_SHARE_WINDOW 6
-#endif
-#ifndef RT_SHARE_OFFERS
-#define RT_SHARE_OFFERS 16
-#endif
-constexpr bool kSpecShare = RT_SPEC_SHARE != 0;
-constexpr int kShareRecords = RT_SHARE_RECORDS;   // a wave posts offers once at most this many records are active
-constexpr int kShareWindow = RT_SHARE_WINDOW;     // jobs in flight per record with offers (local + offers)
-constexpr int kOffers = RT_SHARE_OFFERS;          // offers on a block's board
 static_assert(kSpecWindow >= 1 && kSpecWindow <= 10, "lane table holds 10 slots");
-static_assert(!kSpecShare || (kSpecWindow <= 8 && kShareWindow <= 8 && kShareWindow >= kSpecWindow && kOffers <= 64),
-              "shared runahead: 8-bit table slots");
-// The lanes running jobs f, f+1, ...: slots of a 64-bit table (planes 2 and 3 .w), 6 bits
-// each (a lane), or 8 with RT_SPEC_SHARE: a lane (< 64), an offer (64 + k) or kTabNone (the
-// frontier job was reclaimed from an untaken offer and waits for a lane).
-constexpr int kTabBits = kSpecShare ? 8 : 6;
+// The lanes running jobs f, f+1, ...: 6-bit slots of a 64-bit table (planes 2 and 3 .w).
+// (Round 5's block-shared runahead, RT_SPEC_SHARE, which ran jobs in other waves of the block
+// through an LDS offer board, measured slower, 190.1 vs 187.9 ms, and was
+// deleted in round 6.)
+constexpr int kTabBits = 6;
 constexpr unsigned long long kTabMask = (1ull << kTabBits) - 1ull;
-constexpr int kTabNone = 255;
 __device__ __forceinline__ int spec_tab(unsigned long long t, int q) { return (int)((t >> (kTabBits * q)) & kTabMask); }
 __device__ __forceinline__ unsigned long long spec_tab_set(unsigned long long t, int q, int ln) {
     return (t & ~(kTabMask << (kTabBits * q))) | ((unsigned long long)ln << (kTabBits * q));
-}
-
-// The block's offer board: kOffers entries of 14 words: [0] state, [1] tag (record | epoch <<
-// 6), [2] sample, [3] pixel, [4..6] start state, [7..9] colour, [10..12] end state.  State:
-// kOf* in bits 0-2, kOfCancel (the owner dropped the job while it ran), owner wave in 16-17.
-constexpr uint32_t kOfFree = 0, kOfRes = 1, kOfOpen = 2, kOfTaken = 3, kOfDone = 4, kOfCancel = 8;
-constexpr int kOfWords = 14;
-#if defined(__HIPCC__)
-__shared__ uint32_t spec_board_lds[kSpecShare ? kOffers * kOfWords : 1];
-__shared__ int spec_block_active_lds[1];   // unfinished records of the block
-__shared__ int spec_wave_active_lds[4];    // unfinished records of each wave
-__shared__ int spec_fdone_lds[4];          // per wave: a helper finished one of its offers
-__device__ __forceinline__ uint32_t *spec_board() { return spec_board_lds; }
-__device__ __forceinline__ int *spec_block_active() { return spec_block_active_lds; }
-__device__ __forceinline__ int *spec_fdone() { return spec_fdone_lds; }
-__device__ __forceinline__ int spec_wave_in_block() { return (int)(threadIdx.x >> 6); }
-__device__ __forceinline__ uint32_t board_ld(int i) { return __hip_atomic_load(&spec_board()[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-__device__ __forceinline__ void board_st(int i, uint32_t v) { __hip_atomic_store(&spec_board()[i], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-__device__ __forceinline__ bool board_cas(int i, uint32_t expect, uint32_t want) {
-    return __hip_atomic_compare_exchange_strong(&spec_board()[i], &expect, want, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void block_active_add(int d) {
-    atomicAdd(spec_block_active(), d);
-    atomicAdd(&spec_wave_active_lds[threadIdx.x >> 6], d);
-}
-__device__ __forceinline__ int wave_active() {
-    return __hip_atomic_load(&spec_wave_active_lds[threadIdx.x >> 6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ int block_active() { return __hip_atomic_load(spec_block_active(), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-#else
-// host harness: a board per emulated block (4 waves: mega_slot() / 256)
-inline uint32_t g_spec_board[4096][kOffers * kOfWords];
-inline int g_spec_block_active[4096];
-inline int g_spec_wave_active[4096 * 4];
-inline int g_spec_fdone[4096 * 4];
-inline uint32_t *spec_board() { return g_spec_board[(mega_slot() >> 8) & 4095]; }
-inline int *spec_block_active() { return &g_spec_block_active[(mega_slot() >> 8) & 4095]; }
-inline int *spec_fdone() { return &g_spec_fdone[4 * ((mega_slot() >> 8) & 4095)]; }
-inline int spec_wave_in_block() { return (int)((mega_slot() >> 6) & 3); }
-inline uint32_t board_ld(int i) { return spec_board()[i]; }
-inline void board_st(int i, uint32_t v) { spec_board()[i] = v; }
-inline bool board_cas(int i, uint32_t expect, uint32_t want) {
-    if (spec_board()[i] != expect) return false;
-    spec_board()[i] = want;
-    return true;
-}
-inline void block_active_add(int d) {
-    *spec_block_active() += d;
-    g_spec_wave_active[(mega_slot() >> 6) & (4096 * 4 - 1)] += d;
-}
-inline int block_active() { return *spec_block_active(); }
-inline int wave_active() { return g_spec_wave_active[(mega_slot() >> 6) & (4096 * 4 - 1)]; }
-#endif
-__device__ __forceinline__ uint32_t of_state(uint32_t w) { return w & 7u; }
-__device__ __forceinline__ int of_owner(uint32_t w) { return (int)((w >> 16) & 3u); }
-// The owner no longer needs offer k: free it, or mark it cancelled while a helper runs it.
-__device__ __forceinline__ void offer_cancel(int k) {
-    for (int tries = 0; tries < 4; ++tries) {   // (only the taker races with the owner here)
-        const uint32_t w = board_ld(k * kOfWords);
-        const uint32_t s = of_state(w);
-        if (s == kOfTaken) {
-            if (board_cas(k * kOfWords, w, w | kOfCancel)) return;
-        } else {
-            if (board_cas(k * kOfWords, w, kOfFree)) return;
-        }
-    }
 }
 
 struct SpecView {
@@ -768,38 +682,6 @@ inline void wave_order(const WArr<uint32_t> &key, WArr<int> &srec, WArr<int> &ra
 }
 #endif
 
-// RT_SPEC_SHARE, the main loop's view of the board: did a helper finish one of this wave's
-// offers (a pass adds it), and does another wave have an offer waiting (this wave's idle lanes
-// can take it)?  Every lane calls these (wave-uniform results).
-#if defined(__HIPCC__)
-__device__ __forceinline__ bool spec_fdone_take() {
-    const int w = (int)(threadIdx.x >> 6);
-    const bool h = __hip_atomic_load(&spec_fdone()[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-    if (h) __hip_atomic_store(&spec_fdone()[w], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __any(h);
-}
-__device__ __forceinline__ bool spec_foreign_open() {
-    const int lane = (int)(threadIdx.x & 63), me = (int)(threadIdx.x >> 6);
-    uint32_t w = 0u;
-    if (lane < kOffers) w = __hip_atomic_load(&spec_board()[lane * kOfWords], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __any(lane < kOffers && (w & 7u) == kOfOpen && (int)((w >> 16) & 3u) != me);
-}
-#else
-inline bool spec_fdone_take() {
-    int &h = spec_fdone()[spec_wave_in_block()];
-    const bool v = h != 0;
-    h = 0;
-    return v;
-}
-inline bool spec_foreign_open() {
-    for (int k = 0; k < kOffers; ++k) {
-        const uint32_t w = spec_board()[k * kOfWords];
-        if ((w & 7u) == kOfOpen && (int)((w >> 16) & 3u) != spec_wave_in_block()) return true;
-    }
-    return false;
-}
-#endif
-
 // Position of the i-th (from 0) set bit of m (m has more than i set bits).
 __device__ __forceinline__ int nth_bit(unsigned long long m, int i) {
     int pos = 0;
@@ -811,16 +693,20 @@ __device__ __forceinline__ int popc64(unsigned long long m) { return __builtin_p
 
 // The wave enters its tail (queue empty): every lane's pixel gets a record at this lane; its
 // sample in flight is the frontier job (table slot 0 = this lane), started from the true
-// state (X_f not yet known).
-__device__ __forceinline__ void spec_convert(MegaLane &L, const SpecView &V, int lane) {
-    if (kSpecShare && L.pix >= 0) block_active_add(1);
+// state X_f.  X_f is known from the start for sample 0 (the pixel's seed), so runahead can
+// begin at once; otherwise only once the job ends (the lane's RNG has moved on).
+__device__ __forceinline__ void spec_convert(MegaLane &L, const DevScene &sc, const ShardGeom &g, const SpecView &V,
+                                             int lane) {
     if (L.pix >= 0) {
         const LaneCtr c = lane_ctr(L);
+        const bool x0 = c.s == 0;
+        const Rng X = x0 ? pixel_seed(sc, g, L.pix) : Rng{0u, 0u, 0.f};
         *V.w(0, lane) = make_uint4((uint32_t)L.pix, (uint32_t)c.s, (uint32_t)c.s + 1u, 0u);
-        *V.w(1, lane) = v3_pack(lane_sum(L), kRecActive);
-        *V.w(2, lane) = make_uint4(0u, 0u, 0u, (uint32_t)lane);   // table slot 0: this lane
-        *V.w(3, lane) = make_uint4(0u, 0u, 0u, 0u);
-        *V.w(4, lane) = make_uint4((uint32_t)lane, 0u, 0u, 0u);
+        *V.w(1, lane) = v3_pack(lane_sum(L), x0 ? kRecActive | kRecXf : kRecActive);
+        // X_f, table slot 0 (this lane); the start state of job nxt - 1 (= f); this lane's job
+        *V.w(2, lane) = make_uint4(X.x, X.saved_avail, __float_as_uint(X.saved), (uint32_t)lane);
+        *V.w(3, lane) = make_uint4(X.x, X.saved_avail, __float_as_uint(X.saved), 0u);
+        *V.w(4, lane) = make_uint4((uint32_t)lane, X.x, X.saved_avail, __float_as_uint(X.saved));
     } else {
         *V.w(1, lane) = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -850,30 +736,6 @@ __device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const Sh
     const int lane = (int)(mega_slot() & 63);
     const SpecView V{(uint4 *)st.mid, st.lanes, mega_slot() - lane};
     const uint4 j = *V.w(4, lane);
-    if (kSpecShare && (j.x >> 31)) {   // another wave's offer: result to the board, lane free
-        const int k = (int)(j.x & 0xffu);
-        const Rng E = lane_rng(L);
-        uint32_t *o = spec_board() + k * kOfWords;
-        o[7] = __float_as_uint(color.x);
-        o[8] = __float_as_uint(color.y);
-        o[9] = __float_as_uint(color.z);
-        o[10] = E.x;
-        o[11] = E.saved_avail;
-        o[12] = __float_as_uint(E.saved);
-        for (int tries = 0; tries < 4; ++tries) {
-            const uint32_t w = board_ld(k * kOfWords);
-            if (board_cas(k * kOfWords, w, (w & kOfCancel) ? kOfFree : ((w & ~7u) | kOfDone))) {
-                if (!(w & kOfCancel)) {
-                    spec_fdone()[of_owner(w)] = 1;
-                    RT_SPEC_STAT(9, 1);
-                }
-                break;
-            }
-        }
-        L.pix = -1;
-        L.state = M_IDLE;
-        return;
-    }
     const int r = (int)(j.x & 63u);
     const uint4 a = *V.w(0, r), b = *V.w(1, r);
     const uint32_t t = (uint32_t)c.s;
@@ -889,7 +751,6 @@ __device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const Sh
             out[o + 2] = sum.z;
             *V.w(0, r) = make_uint4(a.x, t + 1u, t + 1u, a.w);
             *V.w(1, r) = v3_pack(sum, 0u);
-            if (kSpecShare) block_active_add(-1);
             RT_SPEC_CHAIN_END(spp);
             L.pix = -1;
             L.state = M_IDLE;
@@ -955,39 +816,22 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         je.put(lane, done ? lane_rng(L) : Rng{0u, 0u, 0.f});
     })
     constexpr int win = kSpecWindow, issue = kSpecIssue;
-    // A. add ended frontier jobs, one per pixel per round, at most `win` rounds (RT_SPEC_SHARE:
-    // as many as jobs can be in flight, so no finished offer is left waiting for an event)
-    constexpr int rounds = kSpecShare ? kShareWindow : win;
-    for (int q = 0; q < rounds; ++q) {
+    // A. add ended frontier jobs, one per pixel per round, at most `win` rounds
+    for (int q = 0; q < win; ++q) {
         WArr<int> prog;
         WAVE_PHASE(lane, {
             const uint32_t m = rm.get(lane);
             const unsigned long long tab = (unsigned long long)th.get(lane) << 32 | tl.get(lane);
             const bool has = (m & kRecActive) && rn.get(lane) > rf.get(lane);
-            const int sl0 = has ? spec_tab(tab, 0) : lane;
-            const int sl1 = has && rn.get(lane) > rf.get(lane) + 1u ? spec_tab(tab, 1) : lane;
-            // (RT_SPEC_SHARE: a slot >= 64 is an offer on the block's board, or kTabNone)
-            const bool off0 = kSpecShare && sl0 >= 64, off1 = kSpecShare && sl1 >= 64;
-            const int j0 = off0 ? lane : sl0, j1 = off1 ? lane : sl1;
+            const int j0 = has ? spec_tab(tab, 0) : lane;
+            const int j1 = has && rn.get(lane) > rf.get(lane) + 1u ? spec_tab(tab, 1) : lane;
             // the frontier job's lane and the next job's lane (shuffles: every lane)
             const int s0 = js.at(j0);
             const uint32_t t0 = jt.at(j0), n0 = jsamp.at(j0);
-            V3 c0 = jc.at(j0);
-            Rng e0 = je.at(j0), y1 = jy.at(j1);
+            const V3 c0 = jc.at(j0);
+            const Rng e0 = je.at(j0), y1 = jy.at(j1);
             const uint32_t tag = (uint32_t)lane | re.get(lane) << 6;
-            bool done0 = !off0 && (s0 == M_DONE_NEW || s0 == M_DONE) && t0 == tag && n0 == rf.get(lane);
-            if (kSpecShare && has && off0 && sl0 < 64 + kOffers) {   // the frontier job is an offer
-                const uint32_t *o = spec_board() + (sl0 - 64) * kOfWords;
-                if (of_state(board_ld((sl0 - 64) * kOfWords)) == kOfDone && o[1] == tag && o[2] == rf.get(lane)) {
-                    done0 = true;
-                    c0 = V3{__uint_as_float(o[7]), __uint_as_float(o[8]), __uint_as_float(o[9])};
-                    e0 = Rng{o[10], o[11], __uint_as_float(o[12])};
-                }
-            }
-            if (kSpecShare && off1 && sl1 < 64 + kOffers) {
-                const uint32_t *o = spec_board() + (sl1 - 64) * kOfWords;
-                y1 = Rng{o[4], o[5], __uint_as_float(o[6])};
-            }
+            const bool done0 = (s0 == M_DONE_NEW || s0 == M_DONE) && t0 == tag && n0 == rf.get(lane);
             int pr = 0;
             if (has && done0) {
                 uint32_t f = rf.get(lane) + 1u, n = rn.get(lane), mm = m | kRecXf;
@@ -996,19 +840,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                 const bool keep = (m & kRecXf) && n > f && rng_same(y1, e0);
                 RT_SPEC_STAT(5, keep ? 1 : 0);
                 RT_SPEC_STAT(4, 1);
-                if (kSpecShare && off0) {   // the offer's result is used: the slot is free again
-                    board_st((sl0 - 64) * kOfWords, kOfFree);
-                    RT_SPEC_STAT(10, 1);
-                }
                 if (!keep && n > f) {   // the runahead past f started from another state
-                    if (kSpecShare)
-                        for (int q = 0; q < (int)(n - f); ++q) {
-                            const int sq = spec_tab(tb, q);
-                            if (sq >= 64 && sq < 64 + kOffers) {
-                                offer_cancel(sq - 64);
-                                RT_SPEC_STAT(13, 1);
-                            }
-                        }
                     re.put(lane, re.get(lane) + 1u);
                     n = f;
                     tb = 0ull;
@@ -1020,7 +852,6 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                     out[o + 1] = sum.y;
                     out[o + 2] = sum.z;
                     mm = 0u;
-                    if (kSpecShare) block_active_add(-1);
                     RT_SPEC_CHAIN_END(spp);
                 }
                 rf.put(lane, f);
@@ -1041,18 +872,9 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
     // job lanes: added, superseded or invalidated jobs end; ended runahead jobs wait
     WAVE_PHASE(lane, {
         MegaLane &L = lanes[lane];
-        const bool foreign = kSpecShare && (jt.get(lane) >> 31) && job_state(js.get(lane));
-        const bool job = job_state(js.get(lane)) && !foreign;
+        const bool job = job_state(js.get(lane));
         const int r = job ? (int)(jt.get(lane) & 63u) : lane;
         const uint32_t fr = rf.at(r), er = re.at(r);
-        if (foreign) {   // another wave's offer: dropped by its owner?
-            const int k = (int)(jt.get(lane) & 0xffu);
-            const uint32_t w = board_ld(k * kOfWords);
-            if ((w & kOfCancel) && board_cas(k * kOfWords, w, kOfFree)) {
-                L.state = M_IDLE;
-                L.pix = -1;
-            }
-        }
         if (job) {
             if ((jt.get(lane) >> 6) != er || jsamp.get(lane) < fr) {
                 L.state = M_IDLE;
@@ -1063,27 +885,9 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         }
     })
     // C1. pixels without a frontier job in flight get one, from the true state X_f
-    // (RT_SPEC_SHARE: also a frontier job still waiting on the board untaken, which is taken
-    // back, or one taken back earlier that found no lane: slot 0 = kTabNone)
     unsigned long long nm = 0, idle = 0;
-    WArr<int> reclaim;
     WAVE_PHASE(lane, {
-        bool need = (rm.get(lane) & kRecActive) && rn.get(lane) == rf.get(lane);
-        int rc = 0;
-        if (kSpecShare && (rm.get(lane) & kRecActive) && rn.get(lane) > rf.get(lane)) {
-            const int sl0 = (int)(tl.get(lane) & (uint32_t)kTabMask);
-            if (sl0 == kTabNone) {
-                rc = 1;
-            } else if (sl0 >= 64 && sl0 < 64 + kOffers) {
-                const uint32_t w = board_ld((sl0 - 64) * kOfWords);
-                if (of_state(w) == kOfOpen && board_cas((sl0 - 64) * kOfWords, w, kOfFree)) {
-                    rc = 1;
-                    RT_SPEC_STAT(12, 1);
-                }
-            }
-            need = need || rc;
-        }
-        reclaim.put(lane, rc);
+        const bool need = (rm.get(lane) & kRecActive) && rn.get(lane) == rf.get(lane);
         WBALLOT(nm, lane, need);
         WBALLOT(idle, lane, lanes[lane].state == M_IDLE);
     })
@@ -1103,12 +907,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         }
         // record side: the k-th needing record got the k-th idle lane
         const int k = popc64(nm & ((1ull << lane) - 1ull));
-        if (kSpecShare && reclaim.get(lane)) {   // only slot 0 changes: the later jobs stay
-            const unsigned long long tb0 = (unsigned long long)th.get(lane) << 32 | tl.get(lane);
-            const unsigned long long tb = spec_tab_set(tb0, 0, k < n_idle ? nth_bit(idle, k) : kTabNone);
-            tl.put(lane, (uint32_t)tb);
-            th.put(lane, (uint32_t)(tb >> 32));
-        } else if (((nm >> lane) & 1ull) && k < n_idle) {
+        if (((nm >> lane) & 1ull) && k < n_idle) {
             rn.put(lane, rf.get(lane) + 1u);
             ry.put(lane, rx.get(lane));
             tl.put(lane, (uint32_t)nth_bit(idle, k));   // slot 0 (no other jobs are in flight)
@@ -1194,71 +993,6 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
             ry.put(lane, yl);
         }
     })
-    if constexpr (kSpecShare) {
-        // C3. a sparse wave posts each record's next job past its local window as an offer
-        // (one per record per pass), for the idle lanes of the block's other waves
-        unsigned long long act = 0, post = 0, fm = 0;
-        const int me = spec_wave_in_block();
-        WAVE_PHASE(lane, { WBALLOT(act, lane, (rm.get(lane) & kRecActive) != 0); })
-        if (popc64(act) <= kShareRecords) {
-            WAVE_PHASE(lane, {
-                const uint32_t m = rm.get(lane), f = rf.get(lane), n = rn.get(lane);
-                WBALLOT(post, lane, (m & kRecActive) && (m & kRecXf) && n > f && (int)(n - f) >= win &&
-                                        (int)(n - f) < kShareWindow && (int)n < spp);
-                WBALLOT(fm, lane, lane < kOffers && of_state(board_ld(lane * kOfWords)) == kOfFree);
-            })
-        }
-        WAVE_PHASE(lane, {
-            const int i = popc64(post & ((1ull << lane) - 1ull));
-            if (((post >> lane) & 1ull) && i < popc64(fm)) {
-                const int k = nth_bit(fm, i);
-                if (board_cas(k * kOfWords, kOfFree, kOfRes | (uint32_t)me << 16)) {
-                    Rng Y = ry.get(lane);
-                    rng_skip_sample(Y, depth, sc.n_lights);
-                    uint32_t *o = spec_board() + k * kOfWords;
-                    const uint32_t f = rf.get(lane), n = rn.get(lane);
-                    o[1] = (uint32_t)lane | re.get(lane) << 6;
-                    o[2] = n;
-                    o[3] = rp.get(lane);
-                    o[4] = Y.x;
-                    o[5] = Y.saved_avail;
-                    o[6] = __float_as_uint(Y.saved);
-                    board_st(k * kOfWords, kOfOpen | (uint32_t)me << 16);
-                    const unsigned long long tb = spec_tab_set((unsigned long long)th.get(lane) << 32 | tl.get(lane),
-                                                               (int)(n - f), 64 + k);
-                    tl.put(lane, (uint32_t)tb);
-                    th.put(lane, (uint32_t)(tb >> 32));
-                    rn.put(lane, n + 1u);
-                    ry.put(lane, Y);
-                    RT_SPEC_STAT(8, 1);
-                }
-            }
-        })
-        // C4. lanes still idle take other waves' offers
-        unsigned long long idle3 = 0, om = 0;
-        WAVE_PHASE(lane, {
-            WBALLOT(idle3, lane, lanes[lane].state == M_IDLE);
-            uint32_t w = 0u;
-            if (lane < kOffers) w = board_ld(lane * kOfWords);
-            WBALLOT(om, lane, lane < kOffers && of_state(w) == kOfOpen && of_owner(w) != me);
-        })
-        WAVE_PHASE(lane, {
-            MegaLane &L = lanes[lane];
-            const int i = popc64(idle3 & ((1ull << lane) - 1ull));
-            if (((idle3 >> lane) & 1ull) && i < popc64(om)) {
-                const int k = nth_bit(om, i);
-                const uint32_t w = board_ld(k * kOfWords);
-                if (of_state(w) == kOfOpen && board_cas(k * kOfWords, w, (w & ~7u) | kOfTaken)) {
-                    const uint32_t *o = spec_board() + k * kOfWords;
-                    const Rng Y{o[4], o[5], __uint_as_float(o[6])};
-                    spec_start(L, sc, g, root, o[3], o[2], Y);
-                    jt.put(lane, 0x80000000u | (uint32_t)k);
-                    jy.put(lane, Y);
-                    RT_SPEC_STAT(11, 1);
-                }
-            }
-        })
-    }
     // store the records and the jobs; can a record still take a job?
     unsigned long long roomy = 0;
     WAVE_PHASE(lane, {
@@ -1271,18 +1005,8 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
         *V.w(4, lane) = make_uint4(jt.get(lane), y.x, y.saved_avail, __float_as_uint(y.saved));
         const uint32_t m = rm.get(lane);
         const uint32_t f = rf.get(lane), n = rn.get(lane);
-        bool rm_room = (m & kRecActive) &&
-                       (n == f || ((m & kRecXf) && (int)(n - f) < win && (int)n < spp));
-        if (kSpecShare && (m & kRecActive) && n > f) {
-            // a frontier job waiting for a lane, on the board untaken, or on the board done
-            // (its helper's signal was taken by this pass): the wave needs another pass
-            const int sl0 = (int)(tl.get(lane) & (uint32_t)kTabMask);
-            if (sl0 == kTabNone) rm_room = true;
-            if (sl0 >= 64 && sl0 < 64 + kOffers) {
-                const uint32_t st0 = of_state(board_ld((sl0 - 64) * kOfWords));
-                if (st0 == kOfOpen || st0 == kOfDone) rm_room = true;
-            }
-        }
+        const bool rm_room = (m & kRecActive) &&
+                             (n == f || ((m & kRecXf) && (int)(n - f) < win && (int)n < spp));
         WBALLOT(roomy, lane, rm_room);
     })
     return roomy != 0;

@@ -37,6 +37,7 @@ using std::isnan;
 // rt_debug_word (code << 56 | value) and clamp the index so the kernel completes.
 #if defined(RT_DEBUG_CHECKS) && defined(__HIPCC__)
 __device__ unsigned long long rt_debug_word;
+__device__ int rt_debug_poison;   // rt_debug_set_poison (rt_device.hip)
 #define RT_CHECK(cond, code, val, fix)                                                                        \
     do {                                                                                                     \
         if (!(cond)) {                                                                                       \
@@ -120,12 +121,6 @@ struct DevScene {
     const uint4 *tex_info;    // texel offset, width, height, channels
     const uint32_t *texels;   // RGBA8
     const float *lut;         // 512: [b] = sRGB decode powf(b / 255.f, 2.2f), [256 + b] = b / 255.f
-    // RT_SOA A/B builds only: the traversal's node and triangle records as
-    // planes of float4 (node: (min, max.x) | (max.yz, a, b) at index 1 + id; triangle:
-    // (v0, U.x) | (U.yz, V.xy) | (V.z, n_geo)), plane strides in float4; null otherwise
-    const float4 *node_soa;
-    const float4 *tri_soa;
-    long long node_plane, tri_plane;
     int n_lights;
     int n_tris, n_nodes, n_meshes;
     int ray_depth;

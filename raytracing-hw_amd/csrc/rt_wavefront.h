@@ -340,6 +340,7 @@ __device__ __forceinline__ void store_qray_inactive(float4 *q, unsigned p) {
 // TravStateU: 53 -> 50 spilled VGPRs, 1145 -> 1132 ms (r03s5).  The runahead kernel keeps
 // TravState: with the shared layout its 8-way shards measured 0.8% slower (205 vs 203 ms mean).
 enum TravPhase : int { TP_NODE = 0, TP_LEAF = 1, TP_POP = 2 };
+static_assert(TP_POP < 4 && kStack < 128, "rt_mega_kernel packs phase in 2 bits and sp in 7 (RT_PACK_TRAV)");
 template <bool SHARED> struct TravFields;
 template <> struct TravFields<false> {
     uint32_t a, b;      // TP_NODE: internal node being entered (b = split axis, a = left child)
@@ -607,9 +608,6 @@ struct LdsStackT {
 // takes; so a leaf of up to 4 triangles is one step, with the reference's winner and local
 // best.  Node lanes run node_step as in trav_step.  Every lane of the wave must call this
 // (active: the lane is traversing); returns true once the lane's stack is empty.
-#ifndef RT_SOA
-#define RT_SOA 0   // 1: SoA node / triangle planes for the coop step (A/B build)
-#endif
 
 // RT_UV_RECOMPUTE: the coop leaf step keeps only (t, triangle) of the closest hit; the
 // shading pass recomputes (u, v) with the same Moller-Trumbore test of that triangle and ray
@@ -683,15 +681,6 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
     RT_CHECK(!at_leaf || T.kend <= (uint32_t)sc.n_tris, 12, T.kend, T.k = T.kend = 1);
     // node lanes: the child pair (issued first; consumed after the leaf exchange)
     float4 q[4];
-#if RT_SOA
-    {   // (A/B layout: two planes, the pair's halves 32 B apart in each)
-        const float4 *p0 = sc.node_soa + 1 + (size_t)(at_node ? T.a : 0u), *p1 = p0 + sc.node_plane;
-        q[0] = p0[0];
-        q[2] = p0[1];
-        q[1] = p1[0];
-        q[3] = p1[1];
-    }
-#else
     if (MASK_LOAD) {
         // (only the node lanes issue the pair loads: the others leave the address unit alone;
         // q is read only by node lanes: no initialisation, which would wait on the registers'
@@ -706,7 +695,6 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
 #pragma unroll
         for (int i = 0; i < 4; ++i) q[i] = p0[i];
     }
-#endif
     // leaf lanes publish (rank = position among the wave's leaf lanes); round b serves
     // ranks b*kCoopLeaves .. (b+1)*kCoopLeaves-1, and a further round runs while at least
     // round_min leaf lanes are left unserved (a wave mostly at leaves: small scenes)
@@ -732,13 +720,8 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
             const float4 a = wf_coop_rec[wave][h][0], b = wf_coop_rec[wave][h][1];
             const uint32_t k = __float_as_uint(a.w) + (uint32_t)j;
             if (k < __float_as_uint(b.w)) {
-#if RT_SOA
-                const float4 *t = sc.tri_soa + (size_t)k;
-                const float4 t0 = t[0], t1 = t[sc.tri_plane], t2 = t[2 * sc.tri_plane];
-#else
                 const float4 *t = sc.tri + 3 * (size_t)k;
                 const float4 t0 = t[0], t1 = t[1], t2 = t[2];
-#endif
                 Ray hr;
                 hr.o = V3{a.x, a.y, a.z};
                 hr.d = V3{b.x, b.y, b.z};

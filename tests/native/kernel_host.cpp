@@ -228,23 +228,12 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     long long queue = 0;
     int live = waves;
     g_rounds = 0;
-    if constexpr (SPEC) {   // blocks of 4 emulated waves: offer boards (RT_SPEC_SHARE)
-        std::memset(rtd::g_spec_board, 0, sizeof rtd::g_spec_board);
-        std::memset(rtd::g_spec_block_active, 0, sizeof rtd::g_spec_block_active);
-        std::memset(rtd::g_spec_wave_active, 0, sizeof rtd::g_spec_wave_active);
-        std::memset(rtd::g_spec_fdone, 0, sizeof rtd::g_spec_fdone);
-    }
     while (live > 0) {
         ++g_rounds;
         if (g_rounds > 50000000ull) {   // (a schedule that stops draining: report, do not hang the test)
             std::fprintf(stderr, "render_mega: no progress after %llu rounds, %d waves live\n",
                          (unsigned long long)g_rounds, live);
             if constexpr (SPEC) {
-                for (int b = 0; b < (waves + 3) / 4; ++b) {
-                    std::fprintf(stderr, " block %d active %d board:", b, rtd::g_spec_block_active[b]);
-                    for (int k = 0; k < rtd::kOffers; ++k) std::fprintf(stderr, " %x", rtd::g_spec_board[b][k * rtd::kOfWords]);
-                    std::fprintf(stderr, "\n");
-                }
                 for (int w = 0; w < waves; ++w) {
                     const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
                     for (int l = 0; l < 64; ++l) {
@@ -286,7 +275,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
             if (exhausted[w] && !tail[w]) {
                 const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
                 rtd::g_mega_slot = (long long)w * 64;
-                for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], V, l);
+                for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], sc, g, V, l);
                 rtd::spec_hint_take();
                 tail[w] = 1;
                 wave_room[w] = 0;
@@ -299,9 +288,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                     fresh |= W[l].state == rtd::M_DONE_NEW;
                     idle |= W[l].state == rtd::M_IDLE;
                 }
-                bool share_pass = false;
-                if constexpr (rtd::kSpecShare) share_pass = rtd::spec_fdone_take() || (idle && rtd::spec_foreign_open());
-                if (fresh || share_pass || (wave_room[w] && idle)) {
+                if (fresh || (wave_room[w] && idle)) {
                     ++g_spec_passes;
                     wave_room[w] = rtd::spec_manage(rtd::SpecLanes{W}, sc, g,
                                                     rtd::SpecView{(uint4 *)st.mid, st.lanes, (long long)w * 64}, spp,
@@ -317,9 +304,6 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                 nt += W[l].state == rtd::M_TRAV || W[l].state == rtd::M_LTRAV;
             }
             if (!any) {
-                rtd::g_mega_slot = (long long)w * 64;
-                if constexpr (SPEC && rtd::kSpecShare)
-                    if (tail[w] && rtd::block_active() > 0) continue;   // a helper (RT_SPEC_SHARE)
                 done[w] = 1;
                 --live;
                 continue;

@@ -104,6 +104,24 @@ def test_errors_are_reported(rt, tmp_path):
     assert lib.rt_tonemap_u8(None, 4, 4, 1, None) == -1
 
 
+def test_unknown_flags_rejected(rt):
+    """Flag bits outside RT_FLAG_ALL fail with RT_ERR_ARG on every render entry, before any
+    device work (a caller built against ABI 5 passing RT_FLAG_POOL = 64 gets an error, not the
+    default schedule)."""
+    s = rt.Scene.load(rtref.scene_path("cornell"), 8, 8, 1)
+    lib = rt.lib()
+    out = np.zeros(8 * 8 * 3, np.float32)
+    rgb = np.zeros(8 * 8 * 3, np.uint8)
+    for bad in (64, 1 << 20, -1):
+        p = rt.RtParams(1, 0, 1, 8, 0, 0, bad, 0, 0)
+        assert lib.rt_render(s.handle, ctypes.byref(p), out.ctypes.data_as(rt._c_f), None) == -1
+        assert b"unknown flag" in lib.rt_last_error()
+        assert lib.rt_render_device(s.handle, ctypes.byref(p), ctypes.c_void_p(1), None, None) == -1
+        assert lib.rt_render_multi(s.handle, ctypes.byref(p), 1, out.ctypes.data_as(rt._c_f), None) == -1
+        assert lib.rt_render_frame(s.handle, ctypes.byref(p), 1, None, rgb.ctypes.data_as(rt._c_b), None, None) == -1
+        assert b"unknown flag" in lib.rt_last_error()
+
+
 def test_scene_from_view_validates(rt):
     a = rtref.ref_arrays(rt, "cornell", 16, 16, 1)
     s = rt.Scene.from_view(a)

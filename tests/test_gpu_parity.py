@@ -434,3 +434,31 @@ def test_idle_lanes_after_another_kernel(gpu):
         _sums(big, 8, count=True, kernel=4)
         out, _ = _sums(small, 3, **kw)
         assert (rtref.bits(out) == rtref.bits(ref)).all(), kw
+
+
+def test_pack_masks_poisoned_lanes(gpu):
+    """The shading pass's packing (rt_device.hip RT_PACK_TRAV) is guarded two ways: the fields
+    are masked, and the index-checked debug build checks phase < 4, state < 8, sp <= kStack
+    before every pack (RT_CHECK 14).  With every lane's phase and stack depth poisoned out of
+    range at the kernel's start (rt_debug_set_poison: the leftovers behind round 5's fault),
+    the lanes that never get a pixel (33x17 = 561 pixels, 768 lanes) carry them into every
+    shading pass: the counting render must still be the reference's sums, and the check must
+    report them.  Debug build only (RT_LIB=raytracing-hw_amd/debug/librt_hw_amd.so)."""
+    if not gpu.is_debug_build():
+        pytest.skip("needs the index-checked debug build (make -C raytracing-hw_amd debug)")
+    small = gpu.Scene.from_view(rtref.ref_arrays(gpu, "cornell", 33, 17, 3))
+    ref = rtref.golden("cornell_sums_33x17x3.rtd")["sums"].reshape(-1, 3)
+    gpu.debug_raise = False
+    try:
+        gpu.debug_take()
+        gpu.debug_set_poison(1)
+        out, st = _sums(small, 3, count=True, natural_order=True)
+        word = gpu.debug_take()
+    finally:
+        gpu.debug_set_poison(0)
+        gpu.debug_raise = True
+    assert st["schedule"] == gpu.SCHED_LANE
+    assert (rtref.bits(out) == rtref.bits(ref)).all()
+    assert word >> 56 == 14, hex(word)
+    out, _ = _sums(small, 3, count=True, natural_order=True)   # unpoisoned: no check fires (raises otherwise)
+    assert (rtref.bits(out) == rtref.bits(ref)).all()

@@ -213,39 +213,6 @@ def test_runahead_priority_orders(rt, tmp_path_factory, prio):
         assert np.array_equal(rtref.bits(out), rtref.bits(want)), name
 
 
-@pytest.mark.parametrize("records,window", [(64, 6), (8, 8), (2, 4)])
-def test_runahead_shared_offers(rt, tmp_path_factory, records, window):
-    """Block-shared runahead (rt_mega.h RT_SPEC_SHARE, the cross-wave job table): waves post
-    jobs past their window as offers on their block's board, other waves of the block run
-    them, and the owners add the results only with the start state proven.  Emulated blocks of
-    4 waves (round-robin), long chains: the plain per-pixel schedule's bits, and offers were
-    posted, taken by other waves and added."""
-    lib = _build_kh(tmp_path_factory, "-DRT_SPEC_SHARE=1", f"-DRT_SHARE_RECORDS={records}",
-                    f"-DRT_SHARE_WINDOW={window}", "-DRT_SPEC_PRIO=1")
-    lib.kh_render_mega_spec.argtypes = lib.kh_render_mega.argtypes
-    lib.kh_render_mega_spec.restype = ctypes.c_int
-    lib.kh_spec_prof.argtypes = [ctypes.c_void_p]
-    used = 0
-    for name, w, h, s, waves in [("sponza_mini", 32, 18, 48, 8), ("cornell_blob", 24, 24, 64, 8),
-                                 ("practice6_1", 40, 30, 12, 12)]:
-        v, keep = _view(rt, name, w, h, s)
-        want = np.zeros((h * w, 3), np.float32)
-        lib.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
-        out = np.zeros((h * w, 3), np.float32)
-        before = np.zeros(16, np.uint64)
-        lib.kh_spec_prof(before.ctypes.data)
-        assert lib.kh_render_mega_spec(ctypes.addressof(v), s, 0, 1, 8, waves, 48, None, out.ctypes.data,
-                                       np.zeros(7, np.uint64).ctypes.data) == 0
-        after = np.zeros(16, np.uint64)
-        lib.kh_spec_prof(after.ctypes.data)
-        d = after - before
-        print(name, "posted", d[8], "taken", d[11], "run to the end", d[9], "added", d[10], "reclaimed", d[12],
-              "cancelled", d[13])
-        assert np.array_equal(rtref.bits(out), rtref.bits(want)), name
-        used += int(d[10])
-    assert used > 0   # some offers were run by another wave and added
-
-
 @pytest.mark.parametrize("name,w,h,s,waves", [("cornell_blob", 48, 48, 4, 2), ("sponza_mini", 64, 36, 4, 3)])
 def test_lane_resident_any_pixel_order(rt, kh, name, w, h, s, waves):
     """The ordered render (rt_device.hip launch_order: queue item p renders pixel order[p])
