@@ -148,13 +148,23 @@ constexpr int kFastMaxChunks = 128;  // fast mode: at most this many work units 
 #define RT_SPEC_PIXELS_PER_LANE 2
 #endif
 constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead kernel up to this many pixels per lane
-// Runahead kernel, shards of at most one pixel per resident lane: the whole resident grid with
-// a static share of the pixels per wave (rt_mega_kernel static_per), instead of one lane per
-// pixel over ceil(pixels / 256) blocks.
-#ifndef RT_SPEC_STATIC
-#define RT_SPEC_STATIC 0
+// Hand-off (round 6): a parity render on the plain kernel (more than kSpecPixelsPerLane pixels
+// per lane) ends its tail in the runahead kernel.  A plain wave whose queue is empty parks its
+// pixels once fewer than kHandoffBelow of its lanes hold one (each at its next sample end, with
+// its RNG state and sum), and a runahead launch over the whole resident grid resumes them
+// (kHandoffPct percent dealt at its start, the rest claimed in the tail): the plain kernel's
+// sparse tail waves, where most lanes idle while a few pixels finish their chains, become
+// runahead records.  Headline frame 1048.3 vs 1061.5 ms on one box, 2-way shards 578.6 vs
+// 580.6 ms, same bits; parking at 48 / 60 held pixels 1049.0 / 1050.8 ms, 70% dealt 1050.2 ms
+// (profiles/r06g_ab.jsonl).  RT_FLAG_NO_RUNAHEAD turns it off with the runahead.
+#ifndef RT_HANDOFF_BELOW
+#define RT_HANDOFF_BELOW 56
 #endif
-constexpr bool kSpecStatic = RT_SPEC_STATIC != 0;
+#ifndef RT_HANDOFF_PCT
+#define RT_HANDOFF_PCT 100
+#endif
+constexpr int kHandoffBelow = RT_HANDOFF_BELOW;
+constexpr int kHandoffPct = RT_HANDOFF_PCT;
 // Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
 // holds at most 64 / k pixels and the grid grows k-fold (lockstep study).
 #ifndef RT_CLAIM_STRIDE
@@ -176,7 +186,9 @@ struct rt_device_scene {
     void *buf = nullptr;               // one allocation holding every scene array
     DevScene ds{};
     unsigned long long *counters = nullptr;  // 16 x u64: [0, 8) the render, [8, 16) the order pre-pass
-    unsigned long long *queue = nullptr;     // 2 x u64: work counters of the render and the pre-pass
+    unsigned long long *queue = nullptr;     // 8 x u64: work counters of the render and the pre-pass, the
+                                             // hand-off's park count (u32), its runahead launch's claims and
+                                             // the address of its park list (rt_mega_kernel `mode`)
     int cu_count = 0;
     // vertex records (lane-resident) / path state and queues (wavefront)
     void *wf_buf = nullptr;
@@ -332,15 +344,25 @@ struct TbAcc {
 // SPEC (parity renders without counting): a wave whose claim finds the queue empty enters its
 // tail and runs speculative sample runahead (rt_mega.h spec_manage) on its idle lanes.  A
 // separate instantiation, so the kernel without it keeps its own register allocation.
-// `static_per` > 0 (SPEC, shards of at most one pixel per resident lane): no queue; wave w of
-// the grid takes queue items [w * static_per, (w + 1) * static_per), its lanes below static_per
-// one each, and enters its tail at once, so the lanes above run runahead jobs from the start.
+// `mode` (0 for the default schedules) packs the hand-off's settings (one kernel argument: the
+// kernel is short of SGPRs, which spill into VGPRs):
+//   bits 0-7   park_below > 0 (plain kernel): a wave whose queue is empty and that holds fewer
+//              than park_below pixels parks them, each at its next sample end, in the park list
+//              at its lane slot (rt_mega.h park_pixel; the list's address in queue[4], read where
+//              used: no register held in the loop);
+//   bits 8-15  resume_pct > 0 (SPEC): the items are that park list's slots (st.n of them); wave
+//              w of the grid takes slots [w * per, (w + 1) * per), its lanes below per one each
+//              (per: resume_pct percent of the slots over the grid's waves, at most 64), skips
+//              the empty ones and enters its tail at once; the slots past the grid's share are
+//              claimed in the tail (rt_mega.h SpecClaim) through the counter at queue + 3.
 template <bool COUNT, bool FAST = false, bool LSPLIT = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SPEC ? kMegaWpeSpec : kMegaWpe, 8)))
 rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out, unsigned long long *counters,
-               unsigned long long *queue, const int *order, unsigned *cost, int cs, int static_per) {
+               unsigned long long *queue, const int *order, unsigned *cost, int cs, int mode) {
     constexpr bool kSpec = SPEC && !COUNT && !FAST && !LSPLIT;
-    const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : g.n_pixels;
+    const int park_below = mode & 255, resume_pct = (mode >> 8) & 255;
+    const uint4 *resume = kSpec && resume_pct > 0 ? (const uint4 *)queue[4] : nullptr;
+    const long long n_items = FAST ? g.n_pixels * (long long)((spp + cs - 1) / cs) : (kSpec && resume) ? st.n : g.n_pixels;
     const int lane = threadIdx.x & 63;
     // sRGB texel-decode table in LDS: the shading's lane-dependent lookups become ds_reads (the
     // linear decode is computed: rt_path.h texel_decode)
@@ -388,12 +410,69 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
     const unsigned long long wt0 = wall_clock64();
     TbAcc tbk;
 #endif
-    if (kSpec && static_per > 0) {
-        const long long p = (rtd::mega_slot() >> 6) * static_per + lane;
-        if (lane < static_per && p < n_items) rtd::mega_assign<COUNT>(L, sc, g, order ? order[p] : (int)p, root, cnt);
-        exhausted = true;
+    // hand-off resume: the slots past waves * per are taken in the tail (rt_mega.h SpecClaim) by
+    // waves below `per` active records
+    rtd::SpecClaim claim{queue + 3, 0, n_items, resume, 0, false};
+    bool park = false;   // (plain kernel, hand-off: this wave parks its pixels)
+    if constexpr (kSpec) {
+        if (resume) {
+            const long long waves = (long long)gridDim.x * (blockDim.x >> 6);
+            const long long dealt = (n_items * resume_pct + 99) / 100;
+            const int per = (int)std::min<long long>(64, std::max<long long>(1, (dealt + waves - 1) / waves));
+            const long long p = (rtd::mega_slot() >> 6) * per + lane;
+            bool xk = false;
+            rtd::Rng xs{0u, 0u, 0.f};
+            if (lane < per && p < n_items) {
+                const rtd::Parked q = rtd::parked(resume, p);
+                if (q.pix != rtd::kNoPark) {
+                    rtd::mega_resume(L, sc, g, q, root);
+                    xk = true;
+                    xs = q.x;
+                }
+            }
+            exhausted = true;
+            claim.base = waves * per;
+            claim.keep = per;
+            claim.open = claim.base < n_items;
+            if (lane == 0) rtd::spec_hint_take();
+            rtd::spec_convert(L, sc, g, rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, lane, xk, xs);
+            tail = true;
+#ifdef RT_MEGA_PROF
+            if (lane == 0) RT_SPEC_STAT(7, 1);
+#endif
+        }
     }
+#if defined(RT_DEBUG_CHECKS)
+    unsigned long long dbg_iter = 0;   // debug builds: a wave looping this long reports and leaves
+#endif
     for (;;) {
+#if defined(RT_DEBUG_CHECKS)
+        if (++dbg_iter > (1ull << 22)) {
+            const unsigned long long w = (unsigned long long)__popcll(__ballot(L.state == rtd::M_TRAV)) |
+                                         (unsigned long long)__popcll(__ballot(L.state == rtd::M_READY)) << 8 |
+                                         (unsigned long long)__popcll(__ballot(L.state == rtd::M_DONE)) << 16 |
+                                         (unsigned long long)__popcll(__ballot(L.state == rtd::M_DONE_NEW)) << 24 |
+                                         (unsigned long long)__popcll(__ballot(L.state == rtd::M_IDLE)) << 32 |
+                                         (unsigned long long)tail << 40 | (unsigned long long)park << 41 |
+                                         (unsigned long long)exhausted << 42 | (unsigned long long)wave_room << 43;
+            RT_CHECK(false, 15, w, (void)0);
+            if constexpr (kSpec) {   // the first such wave prints its lanes and records
+                const rtd::SpecView V{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane};
+                const uint4 a = *V.w(0, lane), b = *V.w(1, lane), c = *V.w(2, lane), d = *V.w(3, lane), j = *V.w(4, lane);
+                if (atomicAdd(&rt_debug_prints, 1u) < 64u)
+                    printf("[stuck] blk %d lane %d state %d pix %d s %d | job tag %u | rec pix %u f %u n %u e %u meta %u tab %08x%08x\n",
+                           (int)blockIdx.x, lane, L.state, L.pix, rtd::lane_ctr(L).s, j.x, a.x, a.y, a.z, a.w, b.w, d.w, c.w);
+            }
+            break;
+        }
+#endif
+        if (!kSpec && !COUNT && !FAST && park) {   // hand-off: lanes idle with a pixel park it
+            if (L.state == rtd::M_IDLE && L.pix >= 0) {
+                rtd::park_pixel((uint4 *)queue[4], rtd::mega_slot_of(L), L.pix, rtd::lane_ctr(L).s, rtd::lane_rng(L),
+                                rtd::lane_sum(L));
+                L.pix = -1;
+            }
+        }
         if (!exhausted) {   // lanes without work take the next items (one atomic per wave)
             const bool need = L.pix < 0 && (kClaimStride == 1 || lane % kClaimStride == 0);
             const unsigned long long m = __ballot(need);
@@ -434,7 +513,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #endif
                     wave_room = rtd::spec_manage(rtd::SpecLanes{L}, sc, g,
                                                  rtd::SpecView{(uint4 *)st.mid, st.lanes, rtd::mega_slot() - lane}, spp,
-                                                 out, root);
+                                                 out, root, claim);
 #ifdef RT_MEGA_PROF
                     if (lane == 0) {
                         RT_SPEC_STAT(0, 1);
@@ -449,6 +528,9 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         } else if (!__any(L.pix >= 0)) {
             break;
         }
+        // hand-off: a wave whose queue is empty and that holds fewer than park_below pixels parks
+        // each of them at its next sample end (rt_mega.h mega_shade)
+        if (!kSpec && park_below > 0 && exhausted && !park) park = __popcll(__ballot(L.pix >= 0)) < park_below;
         const int nr = __popcll(__ballot(L.state == rtd::M_READY || (LSPLIT && L.state == rtd::M_LREADY)));
         const int nt = __popcll(__ballot(L.state == rtd::M_TRAV || (LSPLIT && L.state == rtd::M_LTRAV)));
         const bool shade_now = nr > 0 && (nr >= (kSpec ? kSpecShadeMin : kShadeMin) || nt == 0);
@@ -510,7 +592,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             if (L.state == rtd::M_READY) {
                 L.T.phase = 0;   // dead in a READY lane (its stack is empty: T.sp == 0)
                 L.T.sp = 0;
-                rtd::mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, S, cnt, kSpec && tail);
+                rtd::mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, S, cnt, kSpec && tail, park);
             } else {
                 L.T.phase = (int)(pk & 3u);
                 L.state = (int)((pk >> 2) & 7u);
@@ -527,6 +609,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
         }
         if (kPackTrav && kInvRecompute && !LSPLIT && !kSpec && !FAST && shade_now)
             L.r.inv = rtv::divv(rtd::V3{1.f, 1.f, 1.f}, L.r.d);
+
 #ifdef RT_MEGA_PROF
         {
             const long long t1 = clock64();
@@ -894,7 +977,7 @@ int ensure_device_scene(rt_scene *s, int device) {
     hipError_t e = hipMalloc(&d->buf, b.bytes.size());
     if (e == hipSuccess) e = hipMemcpy(d->buf, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc((void **)&d->counters, 16 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc((void **)&d->queue, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void **)&d->queue, 8 * sizeof(unsigned long long));
     hipDeviceProp_t prop;
     if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) {
@@ -960,6 +1043,11 @@ int ensure_wf(rt_device_scene *d, long long n, int D) {
     w.rec_ab = (float4 *)take(8 * D);
     w.rec_c = take(D);
     w.mid = (float4 *)take(20);   // 5 planes of float4, stride = lane slots (<= cap)
+    {   // the hand-off's park list (32 B per lane slot) is the first ray queue (48 B per slot, unused
+        // by the lane-resident kernels); its address goes where the kernel reads it (queue[4])
+        const unsigned long long park = (unsigned long long)(uintptr_t)d->wf_queue[0];
+        HIP_TRY(hipMemcpy(d->queue + 4, &park, sizeof park, hipMemcpyHostToDevice));
+    }
     d->wf_cap = cap;
     d->wf_D = D;
     return RT_OK;
@@ -1187,14 +1275,10 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                                     : count ? rt_mega_kernel<true>
                                             : spec ? rt_mega_kernel<false, false, false, true> : rt_mega_kernel<false>;
             sched = fast ? RT_SCHED_FAST : lsplit ? RT_SCHED_LIGHT_SPLIT : spec ? RT_SCHED_RUNAHEAD : RT_SCHED_LANE;
-            unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
-            // a shard of at most one pixel per resident lane: the whole resident grid, every wave
-            // with its share of the pixels at once (RT_SPEC_STATIC)
-            int static_per = 0;
-            if (spec && kSpecStatic && kClaimStride == 1 && n_items <= full_blocks * 256) {
-                blocks = (unsigned)full_blocks;
-                static_per = (int)((n_items + 4 * full_blocks - 1) / (4 * full_blocks));
-            }
+            const bool handoff = !spec && !fast && !lsplit && !count && !(p->flags & RT_FLAG_NO_RUNAHEAD) &&
+                                 kClaimStride == 1;
+            if (handoff) sched |= RT_SCHED_RUNAHEAD;
+            const unsigned blocks = persistent_blocks(d, mk, n_items * kClaimStride);
             const long long slots = (long long)blocks * 256;   // lane slots
             // vertex records are addressed with 32-bit byte offsets (rt_path.h LaneRec)
             if ((unsigned long long)slots * (unsigned long long)s->ray_depth * 32ull >= (1ull << 32))
@@ -1204,12 +1288,16 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             rtd::WfState w = d->wf;
             w.n = g.n_pixels;
             w.lanes = slots;   // LaneRec slots (<= the workspace capacity)
+            if (handoff) {   // the park list: every slot "nothing parked"; the runahead launch's claim counter
+                HIP_TRY(hipMemsetAsync(d->wf_queue[0], 0xff, (size_t)slots * 32, stream));
+                HIP_TRY(hipMemsetAsync(d->queue + 3, 0, sizeof(unsigned long long), stream));
+            }
             w.round_min = d->ds.n_nodes < kCoopRoundNodes ? kCoopRoundMinSpec : 65;
             int *order = nullptr;
             if (!fast && !(p->flags & RT_FLAG_NATURAL_ORDER) && (spp >= kOrderMinSpp || (p->flags & RT_FLAG_HEAVY_ORDER))) {
                 // the spread deals one pixel of every cost stratum to each claim of 64 of the
                 // launch's first round (one per wave)
-                rc = launch_order(d, g, stream, 4LL * blocks, static_per > 0 ? static_per : 64, &order);
+                rc = launch_order(d, g, stream, 4LL * blocks, 64, &order);
                 if (rc) return rc;
                 ordered = true;
             }
@@ -1231,8 +1319,17 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
             }
 #endif
             hipLaunchKernelGGL(mk, dim3(blocks), dim3(256), 0, stream, d->ds, g, w, spp, k_out, d->counters, d->queue,
-                               (const int *)order, (unsigned *)nullptr, cs, static_per);
+                               (const int *)order, (unsigned *)nullptr, cs, handoff ? kHandoffBelow : 0);
             HIP_TRY(hipGetLastError());
+            if (handoff) {   // the parked pixels, on the runahead kernel over the whole resident grid
+                rtd::WfState w2 = w;
+                w2.lanes = full_blocks * 256;
+                w2.n = slots;   // the park list's slots
+                hipLaunchKernelGGL((rt_mega_kernel<false, false, false, true>), dim3((unsigned)full_blocks), dim3(256), 0,
+                                   stream, d->ds, g, w2, spp, k_out, d->counters, d->queue, (const int *)nullptr,
+                                   (unsigned *)nullptr, 0, kHandoffPct << 8);
+                HIP_TRY(hipGetLastError());
+            }
             if (fast) {
                 const long long n3 = g.n_pixels * 3;
                 hipLaunchKernelGGL(rt_fast_reduce_kernel, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, stream,
@@ -1306,6 +1403,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                              "cycles in passes/wave=%.3g frontier jobs=%llu runahead jobs=%llu added=%llu "
                              "runahead jobs proven=%llu invalidations=%llu\n", sp[7], sp[7] ? (double)sp[0] / sp[7] : 0.0,
                              sp[0] ? (double)sp[1] / sp[0] : 0.0, (double)sp[1] / pf[7], sp[2], sp[3], sp[4], sp[5], sp[6]);
+                std::fprintf(stderr, "[mega prof] parked pixels claimed in the tail (hand-off): %llu\n", sp[8]);
                 std::fprintf(stderr, "[mega prof] runahead chains: proven share of runahead jobs=%.3f, pixels completed "
                              "in the tail=%llu, mean time per chain link (completion / spp)=%.1f us\n",
                              sp[3] ? (double)sp[5] / (double)sp[3] : 0.0, sp[15], sp[15] ? (double)sp[14] / sp[15] / 100.0 : 0.0);

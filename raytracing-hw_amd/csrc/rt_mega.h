@@ -189,6 +189,23 @@ __device__ __forceinline__ void mega_sample(ML &L, const DevScene &sc, const Sha
     mega_begin<COUNT>(L, root, cnt);
 }
 
+// A parked pixel: (pixel, next sample, start state of that sample, sum so far)
+struct Parked {
+    uint32_t pix, s;
+    Rng x;
+    V3 sum;
+};
+__device__ __forceinline__ Parked parked(const uint4 *park, long long k) {
+    const uint4 a = park[2 * k], b = park[2 * k + 1];
+    Parked q;
+    q.pix = a.x;
+    q.s = a.y;
+    rng_word_unpack(a.z, q.x.x, q.x.saved_avail);
+    q.x.saved = __uint_as_float(a.w);
+    q.sum = V3{__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)};
+    return q;
+}
+
 // The RNG state shard pixel p's sample 0 starts from: minstd_rand seeded with the pixel
 // index (scene.cpp:34, random.cpp:12-18; pixel 0 -> 1).
 __device__ __forceinline__ Rng pixel_seed(const DevScene &sc, const ShardGeom &g, int p) {
@@ -208,6 +225,18 @@ __device__ __forceinline__ void mega_assign(ML &L, const DevScene &sc, const Sha
     L.work0 = cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri;
     lane_rng_set(L, pixel_seed(sc, g, p));
     mega_sample<COUNT>(L, sc, g, root, cnt);
+}
+
+// A parked pixel (hand-off): its next sample from its parked state, onto its parked sum.
+template <class ML>
+__device__ __forceinline__ void mega_resume(ML &L, const DevScene &sc, const ShardGeom &g, const Parked &q,
+                                            const NodeRec &root) {
+    L.pix = (int)q.pix;
+    lane_ctr_set(L, LaneCtr{(int)q.s, 0, 0});
+    lane_sum_set(L, q.sum);
+    lane_rng_set(L, q.x);
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    mega_sample<false>(L, sc, g, root, cnt);
 }
 
 // Fast mode: queue item q = chunk * n_pixels + pixel (every pixel's first chunk, then the
@@ -231,6 +260,20 @@ __device__ __forceinline__ void mega_assign_fast(ML &L, const DevScene &sc, cons
     mega_sample<COUNT, true>(L, sc, g, root, cnt);
 }
 
+// Hand-off (rt_device.hip RT_HANDOFF): a pixel whose next sample is s, whose RNG is at the
+// state sample s starts from and whose sum holds samples 0 .. s-1, written to the park list
+// (one atomic per wave: every lane that parks in the same pass of the wave), and resumed by
+// the runahead kernel from exactly that state: its remaining samples run in order from it and
+// add to that sum, so the bits do not change.
+// The park list: 2 x uint4 per lane slot of the parking launch (pixel, next sample, packed RNG
+// word, normal cache | sum, 0); a slot nobody parked in holds pixel 0xffffffff (the host fills
+// it so before the launch).  Indexed by slot, not by an atomic count: no ballot or atomic in
+// the shading code (that cost the plain kernel 28 more spilled VGPRs).
+constexpr uint32_t kNoPark = 0xffffffffu;
+__device__ __forceinline__ void park_pixel(uint4 *park, long long slot, int pix, int s, const Rng &r, V3 sum) {
+    park[2 * slot] = make_uint4((uint32_t)pix, (uint32_t)s, rng_word_pack(r.x, r.saved_avail), __float_as_uint(r.saved));
+    park[2 * slot + 1] = make_uint4(__float_as_uint(sum.x), __float_as_uint(sum.y), __float_as_uint(sum.z), 0u);
+}
 // Shade the lane's closest hit (one vertex of scene.cpp:85-154); bounce, or end the path:
 // fold, accumulate, next sample or pixel done.
 // Set when a lane of the wave added its sample itself (spec_job_end): its pixel may take
@@ -262,10 +305,13 @@ __device__ void spec_job_end(ML &L, const DevScene &sc, const ShardGeom &g, cons
 
 // `tail` (wave-uniform): the wave runs runahead jobs (spec_manage below); a job's path end
 // goes to spec_job_end instead of the pixel sum in the lane.
+// `park` (wave-uniform; lane-resident kernel, hand-off): a path end that leaves the pixel
+// unfinished stops there (idle, still holding the pixel, for park_pixel) instead of starting
+// its next sample.
 template <bool COUNT, bool FAST = false, class Stack, class ML>
 __device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const ShardGeom &g, const WfState &st,
                                            int spp, float *out, unsigned *cost, const NodeRec &root, Stack &stk,
-                                           Counters &cnt, bool tail = false) {
+                                           Counters &cnt, bool tail = false, bool park = false) {
     LaneRec P{st.rec_ab, st.rec_c, mega_slot_of(L), st.lanes, V3{0.f, 0.f, 0.f}, 0, false};
     Hit h = L.T.best;
     LaneCtr c = lane_ctr(L);
@@ -308,6 +354,11 @@ __device__ __forceinline__ void mega_shade(ML &L, const DevScene &sc, const Shar
         out[3 * o + 2] = sm.z;
         if (COUNT && cost) cost[L.pix] = (unsigned)(cnt.aabb + cnt.tri + cnt.laabb + cnt.ltri - L.work0);
         L.pix = -1;
+        L.state = M_IDLE;
+        return;
+    }
+    if (!COUNT && !FAST && park) {   // (idle, still holding its pixel: the kernel's loop parks it)
+        lane_ctr_set(L, c);
         L.state = M_IDLE;
         return;
     }
@@ -451,7 +502,7 @@ template <bool COUNT, class Stack, class Nodes, bool FAST = false, bool LSPLIT =
 __device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevScene &sc, const ShardGeom &g,
                                              const WfState &st, int spp, float *out, unsigned *cost,
                                              const NodeRec &root, Stack &stk, const Nodes &nodes, Counters &cnt,
-                                             bool tail = false) {
+                                             bool tail = false, bool park = false) {
     if constexpr (LSPLIT) {
         if (shade_now) {
             if (L.state == M_READY || L.state == M_LREADY)
@@ -464,7 +515,7 @@ __device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevSce
         }
     }
     if (shade_now) {
-        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt, tail);
+        if (L.state == M_READY) mega_shade<COUNT, FAST>(L, sc, g, st, spp, out, cost, root, stk, cnt, tail, park);
     } else if (L.state == M_TRAV) {
         if (trav_step<COUNT>(sc, L.r, L.T, stk, nodes, cnt)) L.state = M_READY;
     }
@@ -503,7 +554,8 @@ __device__ __forceinline__ void mega_iterate(ML &L, bool shade_now, const DevSce
 // Diagnostics build (RT_MEGA_PROF): runahead event counts, printed by the launch.
 // [0] management passes [1] their cycles (per wave) [2] frontier jobs issued [3] runahead jobs
 // issued [4] jobs added [5] of them runahead jobs [6] invalidations [7] waves that reached a tail
-// [8]-[13] unused [14] chain-link time sum (pixel completion since its wave's start / spp)
+// [8] parked pixels claimed in the tail (hand-off) [9]-[13] unused [14] chain-link time sum
+// (pixel completion since its wave's start / spp)
 // [15] pixels completed
 #if defined(RT_MEGA_PROF) && defined(__HIPCC__)
 // (per-block LDS sums, added to g_spec_prof once at the end of the kernel: global atomics on
@@ -691,16 +743,40 @@ __device__ __forceinline__ int nth_bit(unsigned long long m, int i) {
 }
 __device__ __forceinline__ int popc64(unsigned long long m) { return __builtin_popcountll(m); }
 
+// Parked pixels a tail wave may still take (the hand-off's runahead launch, rt_mega_kernel
+// `mode`): park-list slot base + c for claim counter value c, below n_items; a wave takes them
+// into free record slots while it has fewer than `keep` active records.
+struct SpecClaim {
+    unsigned long long *queue;
+    long long base, n_items;
+    const uint4 *resume;   // the park list (rt_mega.h parked)
+    int keep;
+    bool open;             // the list may still hold slots (wave-uniform)
+};
+// atomicAdd of the wave (called by every lane; one atomic), its old value in every lane
+__device__ __forceinline__ unsigned long long wave_fetch_add(unsigned long long *q, unsigned k) {
+#if defined(__HIPCC__)
+    unsigned long long b = 0;
+    if ((threadIdx.x & 63) == 0) b = atomicAdd(q, (unsigned long long)k);
+    return __shfl(b, 0, 64);
+#else
+    const unsigned long long b = *q;
+    *q += k;
+    return b;
+#endif
+}
+
 // The wave enters its tail (queue empty): every lane's pixel gets a record at this lane; its
 // sample in flight is the frontier job (table slot 0 = this lane), started from the true
-// state X_f.  X_f is known from the start for sample 0 (the pixel's seed), so runahead can
-// begin at once; otherwise only once the job ends (the lane's RNG has moved on).
+// state X_f.  X_f is known from the start for sample 0 (the pixel's seed) and for a pixel
+// just resumed from the park list (`xk`, X), so runahead can begin at once; otherwise only
+// once the job ends (the lane's RNG has moved on).
 __device__ __forceinline__ void spec_convert(MegaLane &L, const DevScene &sc, const ShardGeom &g, const SpecView &V,
-                                             int lane) {
+                                             int lane, bool xk = false, Rng Xk = Rng{0u, 0u, 0.f}) {
     if (L.pix >= 0) {
         const LaneCtr c = lane_ctr(L);
-        const bool x0 = c.s == 0;
-        const Rng X = x0 ? pixel_seed(sc, g, L.pix) : Rng{0u, 0u, 0.f};
+        const bool x0 = c.s == 0 || xk;
+        const Rng X = xk ? Xk : c.s == 0 ? pixel_seed(sc, g, L.pix) : Rng{0u, 0u, 0.f};
         *V.w(0, lane) = make_uint4((uint32_t)L.pix, (uint32_t)c.s, (uint32_t)c.s + 1u, 0u);
         *V.w(1, lane) = v3_pack(lane_sum(L), x0 ? kRecActive | kRecXf : kRecActive);
         // X_f, table slot 0 (this lane); the start state of job nxt - 1 (= f); this lane's job
@@ -752,6 +828,7 @@ __device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const Sh
             *V.w(0, r) = make_uint4(a.x, t + 1u, t + 1u, a.w);
             *V.w(1, r) = v3_pack(sum, 0u);
             RT_SPEC_CHAIN_END(spp);
+            spec_hint_set();   // (a record slot is free: the next pass may claim a pixel into it)
             L.pix = -1;
             L.state = M_IDLE;
             return;
@@ -783,7 +860,8 @@ __device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const Sh
 // order is heaviest first, rt_order_spread_kernel).  Returns whether a record can still take
 // a job (the wave calls again when a lane is idle).
 __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc, const ShardGeom &g,
-                                            const SpecView &V, int spp, float *out, const NodeRec &root) {
+                                            const SpecView &V, int spp, float *out, const NodeRec &root,
+                                            SpecClaim &claim) {
     const int depth = sc.ray_depth;
     // records (this lane as record holder)
     WArr<uint32_t> rp, rf, rn, re, rm, tl, th;   // tl, th: lane table
@@ -914,6 +992,66 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
             th.put(lane, 0u);
         }
     })
+    // C1b. hand-off: a wave with fewer than claim.keep active records takes parked pixels from
+    // the park list into free record slots, one atomic per wave; the frontier job of each
+    // starts at once on an idle lane, from the parked state: X_f is known, so the record may
+    // take runahead jobs in this same pass.  A pixel's samples still run in order from that
+    // state, and its sum is added in sample order: same bits.
+    if (claim.open) {
+        unsigned long long act = 0, idl = 0;
+        WAVE_PHASE(lane, {
+            WBALLOT(act, lane, (rm.get(lane) & kRecActive) != 0);
+            WBALLOT(idl, lane, lanes[lane].state == M_IDLE);
+        })
+        int want = claim.keep - popc64(act);
+        want = want < popc64(idl) ? want : popc64(idl);
+        if (want > 0) {
+            const long long first = claim.base + (long long)wave_fetch_add(claim.queue, (unsigned)want);
+            const long long left = claim.n_items - first;
+            const int got = left <= 0 ? 0 : (left < (long long)want ? (int)left : want);
+            if (got < want) claim.open = false;
+            const unsigned long long fm = ~act;   // free record slots
+            WArr<int> made;   // (a hand-off claim may find an empty park slot: no record, no job)
+            WAVE_PHASE(lane, {   // record side: the k-th free slot takes item first + k
+                const int k = popc64(fm & ((1ull << lane) - 1ull));
+                made.put(lane, 0);
+                if (((fm >> lane) & 1ull) && k < got) {
+                    const Parked q = parked(claim.resume, first + k);
+                    if (q.pix != kNoPark) {   // (an empty slot: nobody parked there)
+                        made.put(lane, 1);
+                        const Rng X = q.x;
+                        rp.put(lane, q.pix);
+                        rf.put(lane, q.s);
+                        rn.put(lane, q.s + 1u);
+                        re.put(lane, re.get(lane) + 1u);   // (a new epoch: no stale job of the slot matches)
+                        rs.put(lane, q.sum);
+                        rm.put(lane, kRecActive | kRecXf);
+                        rx.put(lane, X);
+                        ry.put(lane, X);
+                        tl.put(lane, (uint32_t)nth_bit(idl, k));   // slot 0: the k-th idle lane
+                        th.put(lane, 0u);
+                        RT_SPEC_STAT(8, 1);
+                    }
+                }
+            })
+            WAVE_PHASE(lane, {   // runner side: the i-th idle lane runs the i-th new record's frontier sample
+                MegaLane &L = lanes[lane];
+                const int i = popc64(idl & ((1ull << lane) - 1ull));
+                const bool run = ((idl >> lane) & 1ull) && i < got;
+                const int r = run ? nth_bit(fm, i) : lane;
+                const uint32_t pix = rp.at(r), e = re.at(r), f = rf.at(r);
+                const Rng X = rx.at(r);
+                const int mk = made.at(r);   // (every lane shuffles: a lane that is off in a
+                                             // ds_bpermute reads as 0 to the lanes that read it)
+                if (run && mk) {
+                    spec_start(L, sc, g, root, pix, f, X);
+                    jt.put(lane, (uint32_t)r | e << 6);
+                    jy.put(lane, X);
+                    RT_SPEC_STAT(2, 1);
+                }
+            })
+        }
+    }
     // C2. runahead: idle lanes take the next jobs of pixels with room in their window
     WArr<int> room, incl;
     unsigned long long idle2 = 0;
@@ -1009,6 +1147,11 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                              (n == f || ((m & kRecXf) && (int)(n - f) < win && (int)n < spp));
         WBALLOT(roomy, lane, rm_room);
     })
+    if (claim.open) {   // a free record slot the next pass may fill
+        unsigned long long act = 0;
+        WAVE_PHASE(lane, { WBALLOT(act, lane, (rm.get(lane) & kRecActive) != 0); })
+        if (popc64(act) < claim.keep) roomy = ~0ull;
+    }
     return roomy != 0;
 }
 

@@ -38,6 +38,7 @@ using std::isnan;
 #if defined(RT_DEBUG_CHECKS) && defined(__HIPCC__)
 __device__ unsigned long long rt_debug_word;
 __device__ int rt_debug_poison;   // rt_debug_set_poison (rt_device.hip)
+__device__ unsigned rt_debug_prints;   // device printf budget of the diagnostics
 #define RT_CHECK(cond, code, val, fix)                                                                        \
     do {                                                                                                     \
         if (!(cond)) {                                                                                       \

@@ -153,6 +153,10 @@ extern "C" void kh_rng(uint32_t seed, int kind, int n, float *out_f, uint32_t *o
 static uint64_t g_spec_passes = 0;   // management passes since the last kh_spec_stats
 static int g_static_per_wave = 0;    // > 0: no queue; wave w takes items [w*P, w*P+P) (study of spare lanes)
 extern "C" void kh_set_static_per_wave(int p) { g_static_per_wave = p; }
+// Hand-off (rt_device.hip RT_HANDOFF): the plain emulation parks (g_park_below > 0) into
+// g_park_list by lane slot; the runahead emulation resumes it (g_resume_pct > 0)
+static int g_park_below = 0, g_resume_pct = 0;
+static std::vector<uint4> g_park_list;
 // div_magic (rt_wavefront.h) against `/` for divisor d: every n below 2^20, the 2^20 values
 // below 2^31, the multiples of d and their neighbours up to 2^31, and `extra` seeded draws;
 // returns the number of mismatches.
@@ -225,7 +229,23 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
     for (auto &L : lanes) { L.pix = -1; L.state = rtd::M_IDLE; }
     std::vector<char> exhausted(waves, 0), done(waves, 0), tail(waves, 0), wave_room(waves, 0);
     rtd::Counters cnt{0, 0, 0, 0, 0, 0, 0};
-    long long queue = 0;
+    unsigned long long queue = 0;
+    rtd::SpecClaim claim{&queue, 0, 0, nullptr, 0, false};
+    // hand-off: parking (plain) / resuming (runahead) as rt_mega_kernel's `mode`
+    const bool parking = !SPEC && !LSPLIT && g_park_below > 0, resuming = SPEC && g_resume_pct > 0;
+    std::vector<char> park(waves, 0);
+    if (parking) g_park_list.assign((size_t)2 * waves * 64, make_uint4(rtd::kNoPark, rtd::kNoPark, rtd::kNoPark, rtd::kNoPark));
+    int res_per = 0;
+    long long res_n = 0;
+    std::vector<char> xk((size_t)waves * 64, 0);
+    std::vector<rtd::Rng> xs((size_t)waves * 64);
+    if (resuming) {
+        res_n = (long long)g_park_list.size() / 2;
+        const long long dealt = (res_n * g_resume_pct + 99) / 100;
+        res_per = (int)std::min<long long>(64, std::max<long long>(1, (dealt + waves - 1) / waves));
+        claim = rtd::SpecClaim{&queue, (long long)waves * res_per, res_n, g_park_list.data(), res_per,
+                               (long long)waves * res_per < res_n};
+    }
     int live = waves;
     g_rounds = 0;
     while (live > 0) {
@@ -249,6 +269,27 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
         for (int w = 0; w < waves; ++w) {
             if (done[w]) continue;
             Lane *W = &lanes[(size_t)w * 64];
+            if (parking && park[w])   // lanes idle with a pixel park it (at their lane slot)
+                for (int l = 0; l < 64; ++l)
+                    if (W[l].state == rtd::M_IDLE && W[l].pix >= 0) {
+                        rtd::g_mega_slot = (long long)w * 64 + l;
+                        rtd::park_pixel(g_park_list.data(), (long long)w * 64 + l, W[l].pix, rtd::lane_ctr(W[l]).s,
+                                        rtd::lane_rng(W[l]), rtd::lane_sum(W[l]));
+                        W[l].pix = -1;
+                    }
+            if (!exhausted[w] && resuming) {   // the park list's slots, res_per per wave
+                for (int l = 0; l < res_per; ++l) {
+                    const long long p = (long long)w * res_per + l;
+                    if (p >= res_n) break;
+                    const rtd::Parked q = rtd::parked(g_park_list.data(), p);
+                    if (q.pix == rtd::kNoPark) continue;
+                    rtd::g_mega_slot = (long long)w * 64 + l;
+                    rtd::mega_resume(W[l], sc, g, q, root);
+                    xk[(size_t)w * 64 + l] = 1;
+                    xs[(size_t)w * 64 + l] = q.x;
+                }
+                exhausted[w] = 1;
+            }
             if (!exhausted[w] && g_static_per_wave > 0) {   // static allotment: wave w renders items [w*P, w*P+P)
                 for (int l = 0; l < 64 && l < g_static_per_wave; ++l) {
                     const long long p = (long long)w * g_static_per_wave + l;
@@ -275,7 +316,11 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
             if (exhausted[w] && !tail[w]) {
                 const rtd::SpecView V{(uint4 *)st.mid, st.lanes, (long long)w * 64};
                 rtd::g_mega_slot = (long long)w * 64;
-                for (int l = 0; l < 64; ++l) rtd::spec_convert(W[l], sc, g, V, l);
+                for (int l = 0; l < 64; ++l) {
+                    rtd::g_mega_slot = (long long)w * 64 + l;
+                    rtd::spec_convert(W[l], sc, g, V, l, xk[(size_t)w * 64 + l] != 0, xs[(size_t)w * 64 + l]);
+                }
+                rtd::g_mega_slot = (long long)w * 64;
                 rtd::spec_hint_take();
                 tail[w] = 1;
                 wave_room[w] = 0;
@@ -292,7 +337,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                     ++g_spec_passes;
                     wave_room[w] = rtd::spec_manage(rtd::SpecLanes{W}, sc, g,
                                                     rtd::SpecView{(uint4 *)st.mid, st.lanes, (long long)w * 64}, spp,
-                                                    out, root);
+                                                    out, root, claim);
                 }
             }
             }
@@ -308,13 +353,21 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                 --live;
                 continue;
             }
+            if (parking && exhausted[w] && !park[w]) {
+                int held = 0;
+                for (int l = 0; l < 64; ++l) held += W[l].pix >= 0;
+                park[w] = held < g_park_below;
+            }
             const bool shade_now = nr > 0 && (nr >= shade_min || nt == 0);
             for (int l = 0; l < 64; ++l) {
                 rtd::ArrayStack S{stacks[(size_t)w * 64 + l].data()};
                 rtd::g_mega_slot = (long long)w * 64 + l;
-                rtd::mega_iterate<!SPEC, decltype(S), decltype(nodes), false, LSPLIT>(W[l], shade_now, sc, g, st, spp,
-                                                                                    out, nullptr, root, S, nodes, cnt,
-                                                                                    (bool)tail[w]);
+                if (parking)   // (parking renders do not count, as on the GPU)
+                    rtd::mega_iterate<false, decltype(S), decltype(nodes), false, LSPLIT>(
+                        W[l], shade_now, sc, g, st, spp, out, nullptr, root, S, nodes, cnt, false, (bool)park[w]);
+                else
+                    rtd::mega_iterate<!SPEC, decltype(S), decltype(nodes), false, LSPLIT>(
+                        W[l], shade_now, sc, g, st, spp, out, nullptr, root, S, nodes, cnt, (bool)tail[w]);
             }
         }
     }
@@ -329,6 +382,26 @@ extern "C" int kh_render_mega(const rt_scene_view *v, int spp, int rank, int wor
 extern "C" int kh_render_mega_spec(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
                                    int shade_min, const int32_t *order, float *out, uint64_t *cnt_out) {
     return render_mega<false, true>(v, spp, rank, world, row_block, waves, shade_min, order, out, cnt_out);
+}
+// Hand-off: the plain emulation over `waves` waves parks its sparse tail waves (fewer than
+// park_below pixels held once the queue is empty), then the runahead emulation over
+// `spec_waves` waves resumes the park list (resume_pct percent dealt at the start).  A
+// non-counting render (cnt_out: the counters of the plain part only).
+extern "C" int kh_render_mega_handoff(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
+                                      int spec_waves, int shade_min, int park_below, int resume_pct,
+                                      const int32_t *order, float *out, uint64_t *cnt_out, uint64_t *parked_out) {
+    g_park_below = park_below;
+    int rc = render_mega<false>(v, spp, rank, world, row_block, waves, shade_min, order, out, cnt_out);
+    g_park_below = 0;
+    if (rc) return rc;
+    uint64_t parked = 0;
+    for (size_t k = 0; k < g_park_list.size(); k += 2) parked += g_park_list[k].x != rtd::kNoPark;
+    *parked_out = parked;
+    g_resume_pct = resume_pct;
+    uint64_t c2[7];
+    rc = render_mega<false, true>(v, spp, rank, world, row_block, spec_waves, shade_min, nullptr, out, c2);
+    g_resume_pct = 0;
+    return rc;
 }
 extern "C" int kh_render_mega_lsplit(const rt_scene_view *v, int spp, int rank, int world, int row_block, int waves,
                                      int shade_min, float *out, uint64_t *cnt_out) {

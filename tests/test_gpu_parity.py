@@ -65,6 +65,11 @@ def test_many_pixels_per_lane_vs_oracle(gpu, oracle):
     lane_n, _ = scene.render_sums(S, runahead=False, natural_order=True)
     assert st0["schedule"] == gpu.SCHED_LANE
     assert np.array_equal(rtref.bits(lane), rtref.bits(lane_n))
+    # the hand-off (the tail's parked pixels resumed by the runahead kernel), both orders
+    for kw in (dict(heavy_order=True), dict(natural_order=True)):
+        ho, sth = scene.render_sums(S, **kw)
+        assert sth["schedule"] == gpu.SCHED_LANE | gpu.SCHED_RUNAHEAD
+        assert np.array_equal(rtref.bits(ho), rtref.bits(lane)), kw
     rng = np.random.default_rng(5)
     for p in rng.choice(W * H, 10, replace=False):
         ref, _, _ = oracle.render(a, S, int(p), int(p) + 1, threads=1)
@@ -376,7 +381,9 @@ def test_schedule_reported(gpu):
     shards, fast mode, the light-split kernel and the wavefront launches."""
     scene = gpu.Scene.load(rtref.scene_path("sponza_mini"), 64, 36, 4)
     big = gpu.Scene.load(rtref.scene_path("sponza_mini"), 1280, 720, 1)
-    assert big.render_sums(1)[1]["schedule"] == gpu.SCHED_LANE
+    # (the plain kernel, its tail handed off to the runahead kernel: rt_device.hip hand-off)
+    assert big.render_sums(1)[1]["schedule"] == gpu.SCHED_LANE | gpu.SCHED_RUNAHEAD
+    assert big.render_sums(1, runahead=False)[1]["schedule"] == gpu.SCHED_LANE
     assert scene.render_sums(4, count=True)[1]["schedule"] == gpu.SCHED_LANE
     assert scene.render_sums(4, rank=1, world=8)[1]["schedule"] == gpu.SCHED_RUNAHEAD
     assert scene.render_sums(4, runahead=False)[1]["schedule"] == gpu.SCHED_LANE
