@@ -16,10 +16,13 @@ value    = scene closest-hit queries (rays, counted in-kernel during warmup; the
 cold_ms_per_step = the very first frame after the scene upload (one-time workspace
            allocation and code-object load included), max over ranks.
 natural_order = the same frame in row-major pixel order (RT_FLAG_NATURAL_ORDER, no pre-pass).
-roofline = rank 0's render kernel.  Default (kernel 0, lane-resident rt_mega_kernel): one
-           launch renders the frame, so achieved = the algorithmic bytes of the whole path
-           (24 B per AABB test + 36 B per triangle test, scene and light BVH,
-           + 156 B per shaded hit) / that launch's duration (HIP events on the launch stream).
+roofline = rank 0's render kernel.  Default (kernel 0, lane-resident rt_mega_kernel): the
+           frame is one launch (the runahead kernel: 4- and 8-way shards) or one launch pair
+           (the plain kernel, then the runahead kernel resuming its parked tail: the hand-off),
+           so achieved = the algorithmic bytes of the whole path (24 B per AABB
+           test + 36 B per triangle test, scene and light BVH, + 156 B per shaded hit) / the
+           render's duration (HIP events on the launch stream around the launch or the pair;
+           the counters of a pair are added).
            With --kernel 4 (wavefront) it is the extend kernel alone: 24 B per AABB test +
            36 B per triangle test + 44 B of ray/hit I/O per ray, per launch / its average
            duration.  Peak: 8 TB/s HBM3E.  `traffic` is the HBM-side bytes per launch from
@@ -66,10 +69,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 B_AABB, B_TRI, B_SHADE = 24, 36, 156
 B_RAY_IO = 24 + 4 + 16     # wf_extend per ray: ray (6 floats) + queue slot in, hit (t, u, v, prim) out
-PROFILE_PREFIX = "r05"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
+PROFILE_PREFIX = "r06"   # profiles/<prefix>_{fetch,write,sq1,sq2}_1080p256.csv of the default command
 # profiles/<prefix>_shard_{fetch,write,sq1,sq2}_w<N>.csv: rank 0's shard of the N-way split
 # (tools/pmc_shard.sh), the counters of an --gpus N line
-SHARD_PROFILE_PREFIX = "r05"
+SHARD_PROFILE_PREFIX = "r06"
 # profiles/<prefix>_fetch_calib.csv: FETCH_SIZE per filled 128-B line for each load shape
 # (tools/fetch_calib.sh)
 CALIB_PREFIX = "r06"
@@ -151,10 +154,15 @@ def cpu_baseline(scene_path, width, height, spp, rows, stride, threads):
 def pmc_mean(path, counter, kname, duration=False):
     """Mean per dispatch of `counter` for the launch of kernel `kname` (its full template list,
     KERNEL_PLAIN or KERNEL_SPEC) in a rocprofv3 --stats PMC summary (None when absent); with
-    duration=True, that pass's average dispatch duration in seconds instead."""
+    duration=True, that pass's average dispatch duration in seconds instead.  `kname` may be a
+    tuple of kernels launched once per frame each (the hand-off: the plain kernel, then the
+    runahead kernel): their means (or durations) are added."""
     import csv
     if not os.path.exists(path):
         return None
+    if isinstance(kname, tuple):
+        vals = [pmc_mean(path, counter, k, duration) for k in kname]
+        return None if any(v is None for v in vals) else sum(vals)
     for row in csv.reader(open(path)):
         if row and row[0].startswith(kname + "(") and row[1] == counter:
             return float(row[5]) * 1e-9 if duration else float(row[4])
@@ -454,9 +462,13 @@ def main():
             avg_s = float(np.sum(ext_ms)) / float(np.sum(ext_n)) / 1e3
             kname = "wf_extend_kernel"
         else:
-            # one launch renders the frame (rank 0's shard): the whole-path model over the launch time
+            # one launch (or the hand-off's pair) renders the frame (rank 0's shard): the whole-path
+            # model over the render time
             bytes_launch, avg_s, launches = bytes_frame, frame_s, 1.0
-            kname = KERNEL_SPEC if sched & rt.SCHED_RUNAHEAD else KERNEL_PLAIN
+            # the plain kernel, the runahead kernel (the 4- and 8-way shards), or both once per
+            # frame (the hand-off: the plain kernel's tail resumed by the runahead kernel)
+            kname = ((KERNEL_PLAIN, KERNEL_SPEC) if sched & rt.SCHED_LANE else KERNEL_SPEC) \
+                if sched & rt.SCHED_RUNAHEAD else KERNEL_PLAIN
         achieved = bytes_launch / avg_s / 1e9
         traffic, traffic_u, traffic_src, issue, traffic_rng, calib = None, None, None, None, None, None
         # the kernel's algorithmic bytes per load shape (node pairs, triangles, texels + shading)
@@ -528,7 +540,8 @@ def main():
                          "traffic_frac": None if traffic_frac is None else round(traffic_frac, 4),
                          "issue": issue,
                          "traffic_source": traffic_src,
-                         "kernel": kname, "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
+                         "kernel": " + ".join(kname) if isinstance(kname, tuple) else kname,
+                         "bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(avg_s * 1e3, 4),
                          "launches_per_frame": launches,
                          "path_frame_bytes": int(bytes_frame), "path_frame_ms": round(frame_s * 1e3, 3),
                          "path_achieved": round(bytes_frame / frame_s / 1e9, 1)},
