@@ -60,7 +60,38 @@ def predictors(depth):
         f.__name__ = f"top{k}"
         return f
 
-    return [always_depth, last, mode, top(2), top(3), top(4)]
+    def majority(hist):
+        # a Boyer-Moore majority vote with a saturating 3-bit count, starting from ray_depth
+        c, k = depth, 0
+        for v in hist:
+            if k == 0:
+                c, k = v, 1
+            elif v == c:
+                k = min(k + 1, 7)
+            else:
+                k -= 1
+        return [c]
+
+    def nibble(prior):
+        # the per-record vote built and measured in round 6: a 4-bit count
+        # per vertex count, all halved when one would pass 15, ray_depth's count starting at
+        # `prior`; the largest count wins, ties to the larger v
+        def f(hist):
+            n = [0] * (depth + 1)
+            n[depth] = prior
+            for v in hist:
+                if n[v] == 15:
+                    n = [x >> 1 for x in n]
+                n[v] += 1
+            best = depth
+            for v in range(depth, -1, -1):
+                if n[v] > n[best]:
+                    best = v
+            return [best]
+        f.__name__ = f"vote_prior{prior}"
+        return f
+
+    return [always_depth, last, mode, majority, nibble(0), nibble(1), nibble(2), nibble(3), top(2), top(3), top(4)]
 
 
 def main():
@@ -68,6 +99,8 @@ def main():
     ap.add_argument("--pixels", type=int, default=128)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--scene-dir", default="/tmp/rt_scenes")
+    ap.add_argument("--select", default="heavy", choices=["heavy", "random"],
+                    help="the heaviest pixels (the 8-way drain's chains) or a uniform sample of the frame")
     args = ap.parse_args()
     import importlib.util
     spec = importlib.util.spec_from_file_location("rt", os.path.join(ROOT, "raytracing-hw_amd", "__init__.py"),
@@ -88,10 +121,13 @@ def main():
     ys, xs = np.mgrid[0:H:12, 0:W:12]
     cand = (ys * W + xs).ravel()
     _, c4 = trace(lib, view, cand, 4)
-    heavy = cand[np.argsort(-c4.sum(1).astype(np.int64))[: args.pixels]]
+    if args.select == "heavy":
+        heavy = cand[np.argsort(-c4.sum(1).astype(np.int64))[: args.pixels]]
+    else:
+        heavy = np.random.default_rng(1).choice(cand, args.pixels, replace=False)
     nv, cost = trace(lib, view, heavy, args.spp)
     hist_v = np.bincount(nv.ravel(), minlength=depth + 1)
-    print("v histogram (heaviest pixels):", (hist_v / hist_v.sum()).round(3).tolist())
+    print(f"v histogram ({args.select} pixels):", (hist_v / hist_v.sum()).round(3).tolist())
     w = cost.astype(np.float64)
     print("cost share by v:", [round(float(w[nv == k].sum() / w.sum()), 3) for k in range(depth + 1)])
     for pred in predictors(depth):
