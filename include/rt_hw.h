@@ -126,8 +126,11 @@ typedef struct {
 /* Parity mode, once the pixel queue is empty, runs the next samples of a wave's unfinished
  * pixels on its idle lanes before their start state is known, and adds only those whose
  * start state is proven equal to the sequential chain's (rt_mega.h, speculative sample
- * runahead): same bits, shorter frame tail.  This flag turns it off.  (Counting renders,
- * count = 1, never use it: their counters are those of the sequential chain.) */
+ * runahead): same bits, shorter frame tail.  A shard of at most two pixels per resident lane
+ * runs on the runahead kernel throughout; a larger one runs on the plain kernel, which hands
+ * its sparse tail waves' pixels to the runahead kernel at a sample boundary (the hand-off:
+ * schedule = RT_SCHED_LANE | RT_SCHED_RUNAHEAD).  This flag turns both off.  (Counting
+ * renders, count = 1, never use it: their counters are those of the sequential chain.) */
 #define RT_FLAG_NO_RUNAHEAD 16
 /* Every defined flag; a call with any other bit set fails with RT_ERR_ARG (e.g. ABI 5's
  * RT_FLAG_POOL = 64, removed in ABI 6). */
@@ -160,7 +163,8 @@ typedef struct {
 
 /* rt_stats.schedule bits: which instantiation of the sample loop ran */
 #define RT_SCHED_LANE 1         /* lane-resident kernel (rt_mega.h), no runahead            */
-#define RT_SCHED_RUNAHEAD 2     /* lane-resident kernel with speculative sample runahead    */
+#define RT_SCHED_RUNAHEAD 2     /* lane-resident kernel with speculative sample runahead
+                                   (both bits: the plain kernel's tail handed to it)        */
 #define RT_SCHED_FAST 4         /* fast mode (RT_FLAG_FAST)                                 */
 #define RT_SCHED_LIGHT_SPLIT 8  /* light-split kernel (RT_FLAG_LIGHT_SPLIT)                 */
 #define RT_SCHED_WAVEFRONT 16   /* wavefront launches (RT_KERNEL_WAVEFRONT)                 */

@@ -1314,6 +1314,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mega_seg), z, 8 * sizeof z[0], 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(rtd::g_spec_prof), z, sizeof z, 0, hipMemcpyHostToDevice, stream));
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wave_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
+                HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(rtd::g_chain_n), z, sizeof(unsigned), 0, hipMemcpyHostToDevice, stream));
                 static const std::vector<unsigned long long> ztb(kTb * kTbN, 0ull);
                 HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tb), ztb.data(), ztb.size() * 8, 0, hipMemcpyHostToDevice, stream));
             }
@@ -1393,6 +1394,50 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                                          alive > 0 ? c[0] / alive : 0.0, c[0] ? (double)c[1] / c[0] : 0.0,
                                          c[0] ? (double)c[2] / c[0] : 0.0, alive > 0 ? c[3] / alive : 0.0,
                                          c[3] ? (double)c[4] / c[3] : 0.0, alive > 0 ? c[5] / alive : 0.0);
+                        }
+                        // the runahead kernel's chain completions: when they end, and where the
+                        // last of them stood in the claim order (0 = the first pixel claimed)
+                        unsigned nc = 0;
+                        HIP_TRY(hipMemcpyFromSymbolAsync(&nc, HIP_SYMBOL(rtd::g_chain_n), sizeof nc, 0, hipMemcpyDeviceToHost, stream));
+                        HIP_TRY(hipStreamSynchronize(stream));
+                        nc = std::min<unsigned>(nc, (unsigned)rtd::kChainRec);
+                        if (nc) {
+                            std::vector<unsigned long long> ct(nc);
+                            std::vector<unsigned> cpx(nc);
+                            HIP_TRY(hipMemcpyFromSymbolAsync(ct.data(), HIP_SYMBOL(rtd::g_chain_t), nc * 8ull, 0, hipMemcpyDeviceToHost, stream));
+                            HIP_TRY(hipMemcpyFromSymbolAsync(cpx.data(), HIP_SYMBOL(rtd::g_chain_pix), nc * 4ull, 0, hipMemcpyDeviceToHost, stream));
+                            const long long np = g.n_pixels;
+                            std::vector<int> rank((size_t)np);
+                            if (order) {
+                                std::vector<int> ord((size_t)np);
+                                HIP_TRY(hipMemcpyAsync(ord.data(), order, (size_t)np * 4, hipMemcpyDeviceToHost, stream));
+                                HIP_TRY(hipStreamSynchronize(stream));
+                                for (long long q = 0; q < np; ++q)
+                                    if (ord[q] >= 0 && ord[q] < np) rank[ord[q]] = (int)q;
+                            } else {
+                                HIP_TRY(hipStreamSynchronize(stream));
+                                for (long long q = 0; q < np; ++q) rank[q] = (int)q;
+                            }
+                            std::vector<unsigned> ix(nc);
+                            for (unsigned q = 0; q < nc; ++q) ix[q] = q;
+                            std::sort(ix.begin(), ix.end(), [&](unsigned a, unsigned b) { return ct[a] < ct[b]; });
+                            auto ms = [&](unsigned q) { return (double)(ct[ix[q]] - t0) / 1e5; };
+                            std::fprintf(stderr, "[mega chains] runahead-kernel chain completions=%u, end ms: p10=%.1f p50=%.1f "
+                                         "p90=%.1f p99=%.1f max=%.1f\n", nc, ms(nc / 10), ms(nc / 2), ms(9 * nc / 10),
+                                         ms((unsigned)(99ull * nc / 100)), ms(nc - 1));
+                            const double fr[4] = {0.5, 0.1, 0.01, 0.001};
+                            for (double f : fr) {
+                                const unsigned k = std::max(1u, (unsigned)(f * nc));
+                                std::vector<double> rr(k);
+                                for (unsigned q = 0; q < k; ++q) {
+                                    const unsigned px = cpx[ix[nc - 1 - q]];
+                                    rr[q] = px < (unsigned)np ? (double)rank[px] / (double)np : -1.0;
+                                }
+                                std::sort(rr.begin(), rr.end());
+                                std::fprintf(stderr, "[mega chains] last %.1f%% (%u chains, from %.1f ms): claim-order position / pixels "
+                                             "p10=%.3f p50=%.3f p90=%.3f\n", 100.0 * f, k, ms(nc - k), rr[k / 10], rr[k / 2],
+                                             rr[9 * k / 10]);
+                            }
                         }
                     }
                 }

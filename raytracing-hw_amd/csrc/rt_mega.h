@@ -566,16 +566,28 @@ __shared__ unsigned long long spec_prof_lds[16];
 // chain links: a pixel's completion time since its wave's start (wall clock, 100 MHz) / spp,
 // summed in [14] (count in [15]); the wave's start time is set by the kernel
 __shared__ unsigned long long spec_wave_t0_lds[4];
-#define RT_SPEC_CHAIN_END(spp) \
+// every chain's completion (wall clock, pixel), for the tail study of the launch's print
+constexpr int kChainRec = 1 << 20;
+__device__ unsigned long long g_chain_t[kChainRec];
+__device__ unsigned int g_chain_pix[kChainRec];
+__device__ unsigned int g_chain_n;
+#define RT_SPEC_CHAIN_END(spp, pix) \
     RT_SPEC_STAT(14, (wall_clock64() - ::rtd::spec_wave_t0_lds[threadIdx.x >> 6]) / (unsigned long long)(spp)); \
-    RT_SPEC_STAT(15, 1)
+    RT_SPEC_STAT(15, 1); \
+    { \
+        const unsigned ci_ = atomicAdd(&::rtd::g_chain_n, 1u); \
+        if (ci_ < (unsigned)::rtd::kChainRec) { \
+            ::rtd::g_chain_t[ci_] = wall_clock64(); \
+            ::rtd::g_chain_pix[ci_] = (unsigned)(pix); \
+        } \
+    }
 #elif !defined(__HIPCC__)
 inline unsigned long long g_spec_prof[16];   // host test harness
 #define RT_SPEC_STAT(k, v) (::rtd::g_spec_prof[k] += (unsigned long long)(v))
-#define RT_SPEC_CHAIN_END(spp) do { } while (0)
+#define RT_SPEC_CHAIN_END(spp, pix) do { } while (0)
 #else
 #define RT_SPEC_STAT(k, v) do { } while (0)
-#define RT_SPEC_CHAIN_END(spp) do { } while (0)
+#define RT_SPEC_CHAIN_END(spp, pix) do { } while (0)
 #endif
 
 // Record meta (plane 1 .w): bit 0 active, bit 1 X_f known (for a pixel that entered the tail
@@ -827,7 +839,7 @@ __device__ __forceinline__ void spec_job_end(ML &L, const DevScene &sc, const Sh
             out[o + 2] = sum.z;
             *V.w(0, r) = make_uint4(a.x, t + 1u, t + 1u, a.w);
             *V.w(1, r) = v3_pack(sum, 0u);
-            RT_SPEC_CHAIN_END(spp);
+            RT_SPEC_CHAIN_END(spp, a.x);
             spec_hint_set();   // (a record slot is free: the next pass may claim a pixel into it)
             L.pix = -1;
             L.state = M_IDLE;
@@ -930,7 +942,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                     out[o + 1] = sum.y;
                     out[o + 2] = sum.z;
                     mm = 0u;
-                    RT_SPEC_CHAIN_END(spp);
+                    RT_SPEC_CHAIN_END(spp, rp.get(lane));
                 }
                 rf.put(lane, f);
                 rn.put(lane, n);
