@@ -156,7 +156,7 @@ constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead 
 // sparse tail waves, where most lanes idle while a few pixels finish their chains, become
 // runahead records.  Headline frame 1048.3 vs 1061.5 ms on one box, 2-way shards 578.6 vs
 // 580.6 ms, same bits; parking at 48 / 60 held pixels 1049.0 / 1050.8 ms, 70% dealt 1050.2 ms
-// (profiles/r06g_ab.jsonl).  RT_FLAG_NO_RUNAHEAD turns it off with the runahead.
+// (profiles/r06g_handoff_ab.jsonl).  RT_FLAG_NO_RUNAHEAD turns it off with the runahead.
 #ifndef RT_HANDOFF_BELOW
 #define RT_HANDOFF_BELOW 56
 #endif
