@@ -163,8 +163,16 @@ constexpr long long kSpecPixelsPerLane = RT_SPEC_PIXELS_PER_LANE;   // runahead 
 #ifndef RT_HANDOFF_PCT
 #define RT_HANDOFF_PCT 100
 #endif
+// RT_HANDOFF_SPREAD: the runahead launch deals the parked pixels with the most work left
+// ((samples left) x (pre-pass estimate)) one per wave, instead of in park-list slot order,
+// where a plain wave's consecutive claims (the last pixels of the order, those that end the
+// frame) sit together and share one wave's idle lanes.
+#ifndef RT_HANDOFF_SPREAD
+#define RT_HANDOFF_SPREAD 1
+#endif
 constexpr int kHandoffBelow = RT_HANDOFF_BELOW;
 constexpr int kHandoffPct = RT_HANDOFF_PCT;
+constexpr bool kHandoffSpread = RT_HANDOFF_SPREAD != 0;
 // Diagnostics (A/B builds only): only every k-th lane of a wave claims pixels, so a wave
 // holds at most 64 / k pixels and the grid grows k-fold (lockstep study).
 #ifndef RT_CLAIM_STRIDE
@@ -412,7 +420,8 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
 #endif
     // hand-off resume: the slots past waves * per are taken in the tail (rt_mega.h SpecClaim) by
     // waves below `per` active records
-    rtd::SpecClaim claim{queue + 3, 0, n_items, resume, 0, false};
+    // (the resume map's address in queue[5], 0 = slot order: read where used)
+    rtd::SpecClaim claim{queue + 3, 0, n_items, resume, 0, false, resume ? (const int *)queue[5] : nullptr};
     bool park = false;   // (plain kernel, hand-off: this wave parks its pixels)
     if constexpr (kSpec) {
         if (resume) {
@@ -423,7 +432,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             bool xk = false;
             rtd::Rng xs{0u, 0u, 0.f};
             if (lane < per && p < n_items) {
-                const rtd::Parked q = rtd::parked(resume, p);
+                const rtd::Parked q = rtd::parked_item(resume, claim.ridx, p);
                 if (q.pix != rtd::kNoPark) {
                     rtd::mega_resume(L, sc, g, q, root);
                     xk = true;
@@ -688,6 +697,23 @@ __global__ void __launch_bounds__(256) rt_order_spread_kernel(const int *sorted,
     }
     order[q] = sorted[r];
 }
+
+// Hand-off, between the two launches: the sort keys of the park list's slots, the work a
+// parked pixel has left as (samples left) x (its pre-pass estimate + 1); 0 for an empty slot.
+// The slots sorted by it, heaviest first, then go through rt_order_spread_kernel, so that the
+// runahead launch deals the parked pixels with the most work left one per wave.
+__global__ void __launch_bounds__(256) rt_park_keys_kernel(const uint4 *park, long long n, int spp, const unsigned *est,
+                                                           unsigned *keys, int *ids) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rtd::Parked q = rtd::parked(park, i);
+    unsigned long long k = 0;
+    if (q.pix != rtd::kNoPark) k = (unsigned long long)(spp - (int)q.s) * ((unsigned long long)est[q.pix] + 1ull);
+    keys[i] = k > 0xffffffffull ? 0xffffffffu : (unsigned)k;
+    ids[i] = (int)i;
+}
+// One 64-bit word, in stream order (the resume map's address in the queue block).
+__global__ void rt_set_u64_kernel(unsigned long long *dst, unsigned long long v) { *dst = v; }
 
 // ------------------------------------------------------------------------ wavefront (kernel 4)
 // (rt_wavefront.h) init -> { extend ; shade } until every slot has finished its samples.
@@ -1323,6 +1349,36 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                                (const int *)order, (unsigned *)nullptr, cs, handoff ? kHandoffBelow : 0);
             HIP_TRY(hipGetLastError());
             if (handoff) {   // the parked pixels, on the runahead kernel over the whole resident grid
+                // with the pixel order's estimates at hand, the slots heaviest first (work left),
+                // spread one per wave (RT_HANDOFF_SPREAD); else slot order
+                unsigned long long map = 0;
+                if (kHandoffSpread && ordered) {
+                    const size_t arr = (((size_t)g.n_pixels * 4 + 255) / 256) * 256;
+                    uint8_t *b = (uint8_t *)d->order_buf;
+                    const unsigned *est = (const unsigned *)b;   // launch_order's filtered costs
+                    unsigned *keys = (unsigned *)(b + arr), *keys_sorted = (unsigned *)(b + 4 * arr);
+                    int *ids = (int *)(b + 2 * arr), *ids_sorted = (int *)(b + 3 * arr), *map_p = (int *)(b + arr);
+                    void *tmp = b + 5 * arr;
+                    size_t tmp_bytes = 0;
+                    HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp_bytes, (unsigned *)nullptr,
+                                                                         (unsigned *)nullptr, (int *)nullptr, (int *)nullptr,
+                                                                         (int)slots, 0, 32, stream));
+                    const unsigned nbs = (unsigned)((slots + 255) / 256);
+                    hipLaunchKernelGGL(rt_park_keys_kernel, dim3(nbs), dim3(256), 0, stream, (const uint4 *)d->wf_queue[0],
+                                       slots, spp, est, keys, ids);
+                    HIP_TRY(hipGetLastError());
+                    HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, keys, keys_sorted, ids, ids_sorted,
+                                                                         (int)slots, 0, 32, stream));
+                    // (the runahead launch's static deal: `per` slots to each of its waves, as in the kernel)
+                    const long long waves2 = 4LL * full_blocks, dealt = (slots * kHandoffPct + 99) / 100;
+                    const long long per2 = std::min<long long>(64, std::max<long long>(1, (dealt + waves2 - 1) / waves2));
+                    hipLaunchKernelGGL(rt_order_spread_kernel, dim3(nbs), dim3(256), 0, stream, (const int *)ids_sorted,
+                                       map_p, slots, waves2, per2);
+                    HIP_TRY(hipGetLastError());
+                    map = (unsigned long long)(uintptr_t)map_p;
+                }
+                hipLaunchKernelGGL(rt_set_u64_kernel, dim3(1), dim3(1), 0, stream, d->queue + 5, map);
+                HIP_TRY(hipGetLastError());
                 rtd::WfState w2 = w;
                 w2.lanes = full_blocks * 256;
                 w2.n = slots;   // the park list's slots

@@ -764,7 +764,13 @@ struct SpecClaim {
     const uint4 *resume;   // the park list (rt_mega.h parked)
     int keep;
     bool open;             // the list may still hold slots (wave-uniform)
+    const int *ridx;       // item -> park-list slot (the spread of the parked pixels), or null
 };
+// Item p of the resume launch: the parked pixel in slot ridx[p] (the host's spread: the
+// pixels with the most work left dealt one per wave) or, without a map, in slot p.
+__device__ __forceinline__ Parked parked_item(const uint4 *park, const int *ridx, long long p) {
+    return parked(park, ridx ? (long long)ridx[p] : p);
+}
 // atomicAdd of the wave (called by every lane; one atomic), its old value in every lane
 __device__ __forceinline__ unsigned long long wave_fetch_add(unsigned long long *q, unsigned k) {
 #if defined(__HIPCC__)
@@ -1028,7 +1034,7 @@ __device__ __forceinline__ bool spec_manage(SpecLanes lanes, const DevScene &sc,
                 const int k = popc64(fm & ((1ull << lane) - 1ull));
                 made.put(lane, 0);
                 if (((fm >> lane) & 1ull) && k < got) {
-                    const Parked q = parked(claim.resume, first + k);
+                    const Parked q = parked_item(claim.resume, claim.ridx, first + k);
                     if (q.pix != kNoPark) {   // (an empty slot: nobody parked there)
                         made.put(lane, 1);
                         const Rng X = q.x;

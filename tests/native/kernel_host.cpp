@@ -157,6 +157,11 @@ extern "C" void kh_set_static_per_wave(int p) { g_static_per_wave = p; }
 // g_park_list by lane slot; the runahead emulation resumes it (g_resume_pct > 0)
 static int g_park_below = 0, g_resume_pct = 0;
 static std::vector<uint4> g_park_list;
+// RT_HANDOFF_SPREAD (rt_device.hip): the resume launch deals the slots heaviest first (work
+// left; the harness has no pre-pass estimate, so samples left), spread one per wave
+static int g_handoff_spread = 1;
+extern "C" void kh_set_handoff_spread(int on) { g_handoff_spread = on; }
+static std::vector<int> g_ridx;
 // div_magic (rt_wavefront.h) against `/` for divisor d: every n below 2^20, the 2^20 values
 // below 2^31, the multiples of d and their neighbours up to 2^31, and `extra` seeded draws;
 // returns the number of mismatches.
@@ -244,7 +249,26 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
         const long long dealt = (res_n * g_resume_pct + 99) / 100;
         res_per = (int)std::min<long long>(64, std::max<long long>(1, (dealt + waves - 1) / waves));
         claim = rtd::SpecClaim{&queue, (long long)waves * res_per, res_n, g_park_list.data(), res_per,
-                               (long long)waves * res_per < res_n};
+                               (long long)waves * res_per < res_n, nullptr};
+        if (g_handoff_spread) {   // rt_park_keys_kernel, the descending sort, rt_order_spread_kernel
+            std::vector<std::pair<unsigned, int>> kv((size_t)res_n);
+            for (long long i = 0; i < res_n; ++i) {
+                const rtd::Parked q = rtd::parked(g_park_list.data(), i);
+                kv[(size_t)i] = {q.pix == rtd::kNoPark ? 0u : (unsigned)(spp - (int)q.s), (int)i};
+            }
+            std::stable_sort(kv.begin(), kv.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+            const long long per = res_per, m = std::min<long long>(res_n, (long long)waves * per), a = m / per, b = m % per;
+            g_ridx.resize((size_t)res_n);
+            for (long long q = 0; q < res_n; ++q) {
+                long long r = q;
+                if (q < m) {
+                    const long long gi = q / per, j = q % per;
+                    r = j * a + (j < b ? j : b) + gi;
+                }
+                g_ridx[(size_t)q] = kv[(size_t)r].second;
+            }
+            claim.ridx = g_ridx.data();
+        }
     }
     int live = waves;
     g_rounds = 0;
@@ -281,7 +305,7 @@ static int render_mega(const rt_scene_view *v, int spp, int rank, int world, int
                 for (int l = 0; l < res_per; ++l) {
                     const long long p = (long long)w * res_per + l;
                     if (p >= res_n) break;
-                    const rtd::Parked q = rtd::parked(g_park_list.data(), p);
+                    const rtd::Parked q = rtd::parked_item(g_park_list.data(), claim.ridx, p);
                     if (q.pix == rtd::kNoPark) continue;
                     rtd::g_mega_slot = (long long)w * 64 + l;
                     rtd::mega_resume(W[l], sc, g, q, root);

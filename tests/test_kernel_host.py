@@ -316,15 +316,19 @@ def test_runahead_with_spare_lanes(rt, kh, per_wave):
     assert rounds[1] < rounds[0]
 
 
+@pytest.mark.parametrize("spread", [1, 0])
 @pytest.mark.parametrize("name,w,h,s,waves,spec_waves,below,pct", [
     ("sponza_mini", 48, 27, 6, 6, 4, 48, 100), ("sponza_mini", 48, 27, 6, 6, 3, 32, 60),
     ("cornell_blob", 40, 40, 8, 8, 8, 56, 100), ("practice6_1", 40, 30, 6, 5, 2, 40, 50)])
-def test_handoff_matches_per_pixel(rt, kh, name, w, h, s, waves, spec_waves, below, pct):
+def test_handoff_matches_per_pixel(rt, kh, name, w, h, s, waves, spec_waves, below, pct, spread):
     """Hand-off (rt_device.hip RT_HANDOFF): the plain lane-resident kernel parks the pixels of
     its sparse tail waves at a sample boundary (rt_mega.h park_pixel: pixel, next sample, RNG
     state, sum so far, by lane slot), and the runahead kernel resumes them (static allotment of
-    `pct` percent, the rest claimed in the tail).  Same bits as the per-pixel schedule, and
-    pixels were parked."""
+    `pct` percent, the rest claimed in the tail), in park-list slot order or (`spread`,
+    RT_HANDOFF_SPREAD) through the map that deals the pixels with the most work left one per
+    wave.  Same bits as the per-pixel schedule, and pixels were parked."""
+    kh.kh_set_handoff_spread.argtypes = [ctypes.c_int]
+    kh.kh_set_handoff_spread(spread)
     v, keep = rt.make_view(rtref.ref_arrays(rt, name, w, h, s))
     want = np.zeros((h * w, 3), np.float32)
     kh.kh_render(ctypes.addressof(v), s, 0, w * h, want.ctypes.data, np.zeros(6, np.uint64).ctypes.data)
@@ -334,6 +338,7 @@ def test_handoff_matches_per_pixel(rt, kh, name, w, h, s, waves, spec_waves, bel
     parked = np.zeros(1, np.uint64)
     assert kh.kh_render_mega_handoff(ctypes.addressof(v), s, 0, 1, 8, waves, spec_waves, 48, below, pct, None,
                                      out.ctypes.data, np.zeros(7, np.uint64).ctypes.data, parked.ctypes.data) == 0
+    kh.kh_set_handoff_spread(1)
     assert np.array_equal(rtref.bits(out), rtref.bits(want))
     assert parked[0] > 0
 
