@@ -1352,7 +1352,7 @@ int launch(rt_scene *s, const rt_params *p, float *d_out, hipStream_t stream, rt
                 // with the pixel order's estimates at hand, the slots heaviest first (work left),
                 // spread one per wave (RT_HANDOFF_SPREAD); else slot order
                 unsigned long long map = 0;
-                if (kHandoffSpread && ordered) {
+                if (kHandoffSpread && ordered && slots <= g.n_pixels) {   // (the order buffer holds n_pixels per array)
                     const size_t arr = (((size_t)g.n_pixels * 4 + 255) / 256) * 256;
                     uint8_t *b = (uint8_t *)d->order_buf;
                     const unsigned *est = (const unsigned *)b;   // launch_order's filtered costs
