@@ -669,10 +669,28 @@ struct NoHook {
 // kernel takes it and the plain kernel does not.  Two other request shapes were measured and
 // removed: quad-cooperative pair loads with a DPP transpose (1259 ms, 8-way 233 ms) and 36-B
 // triangle loads (1132-1137 ms, 8-way 204 ms: neutral).
+// Leaf deferral (the caller passes `leaf_defer`: the runahead kernel).  A step whose wave has
+// fewer than RT_LEAF_DEFER leaf lanes, and some node lanes, leaves its leaf lanes for the next
+// step (at most RT_LEAF_DEFER_MAX steps in a row), so that the coop step's three triangle
+// loads and its triangle test run for more leaves at once; a leaf lane's triangles, their
+// order and its closest hit are unchanged (same bits), it only reaches them a step or two
+// later.  8-way shards of the headline frame, slowest / mean (profiles/r06s, r06t, two calls,
+// two runs each): below 6 with at most 3 in a row 176.3-176.9 / 174.9-175.4 ms, below 6 with
+// at most 2 176.3-177.6 / 175.3-175.5, below 4 / 5 / 7 / 8 / 10 179.2-180.1 / 178.4-179.2 /
+// 177.1-178.4 / 177.1-177.9 / 179.0-179.7, against 183.5-184.5 / 181.5-182.3 without.  The
+// plain kernel (1 GPU) does not defer: below 2 / 3 it measured 1073 / 1064 ms against 1048
+// (profiles/r06r_leaf_defer_ab.jsonl), below 4 equal.
+#ifndef RT_LEAF_DEFER
+#define RT_LEAF_DEFER 6
+#endif
+#ifndef RT_LEAF_DEFER_MAX
+#define RT_LEAF_DEFER_MAX 3
+#endif
+constexpr int kLeafDefer = RT_LEAF_DEFER, kLeafDeferMax = RT_LEAF_DEFER_MAX;
 template <bool COUNT, int kCoopLeaves, bool MASK_LOAD, class Stack, class Nodes, class TS, class Hook = NoHook>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TS &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active, int round_min,
-                                               const Hook &hook = Hook{}) {
+                                               const Hook &hook = Hook{}, int *leaf_defer = nullptr) {
     static_assert(kCoopLeaves >= 1 && kCoopLeaves <= 16, "4 helper lanes per leaf lane");
     __shared__ float4 wf_coop_rec[4][kCoopLeaves][2];   // per wave: (origin, k), (direction, kend)
     const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
@@ -701,7 +719,16 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
     const unsigned long long lm = __ballot(at_leaf);
     const int n_leaf = __popcll(lm);
     const int lrank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-    for (int base = 0; base < n_leaf; base += kCoopLeaves) {   // (wave-uniform)
+    bool skip_leaves = false;   // (wave-uniform)
+    if (kLeafDefer > 0 && leaf_defer) {
+        if (n_leaf > 0 && n_leaf < kLeafDefer && *leaf_defer < kLeafDeferMax && __ballot(at_node) != 0ull) {
+            skip_leaves = true;
+            ++*leaf_defer;
+        } else {
+            *leaf_defer = 0;
+        }
+    }
+    for (int base = 0; !skip_leaves && base < n_leaf; base += kCoopLeaves) {   // (wave-uniform)
         if (base > 0 && n_leaf - base < round_min) break;
         const int rank = lrank - base;
         const bool served = at_leaf && rank >= 0 && rank < kCoopLeaves;
