@@ -63,8 +63,12 @@ constexpr int kMegaWpeSpec = RT_SPEC_WPE;
 // at 32 against 297-299 at 48 (profiles/r02_tail_ab.jsonl).
 // Round 5, with the runahead priority (rt_mega.h RT_SPEC_PRIO): 48 READY lanes, 8-way shards
 // 187.2 max / 185.6 mean ms against 188.2-188.5 / 186.9-187.5 at 40 (profiles/r05f_prio_variants_ab.jsonl).
+// Round 6, with leaf deferral (rt_wavefront.h RT_LEAF_DEFER): 44 READY lanes, 12 coop leaf
+// records and at most 4 deferrals in a row, slowest 8-way shard 174.4-175.8 / mean 173.2-173.7
+// ms against 176.1-176.5 / 174.4-174.9 at 48, 16 and 3 (profiles/r06w_spec_tuning_ab.jsonl,
+// three runs each; 52 lanes 179.6-179.8 in r06v).
 #ifndef RT_SPEC_SHADE_MIN
-#define RT_SPEC_SHADE_MIN 48
+#define RT_SPEC_SHADE_MIN 44
 #endif
 constexpr int kSpecShadeMin = RT_SPEC_SHADE_MIN;   // the runahead kernel's batch threshold
 constexpr int kShadeMin = RT_SHADE_MIN;   // a wave shades once this many lanes are READY (or none traverses)
@@ -95,7 +99,7 @@ constexpr bool kInvRecompute = RT_INV_RECOMPUTE != 0;
 #endif
 constexpr int kCoopLeavesPlain = RT_COOP_LEAVES;
 #ifndef RT_SPEC_COOP_LEAVES
-#define RT_SPEC_COOP_LEAVES 16
+#define RT_SPEC_COOP_LEAVES 12   // (16 until round 6's leaf deferral: see RT_SPEC_SHADE_MIN)
 #endif
 constexpr int kCoopLeavesSpec = RT_SPEC_COOP_LEAVES;   // the runahead kernel's coop leaf records per wave
 // The runahead kernel's coop step issues the child-pair loads from node lanes only

@@ -677,14 +677,15 @@ struct NoHook {
 // later.  8-way shards of the headline frame, slowest / mean (profiles/r06s, r06t, two calls,
 // two runs each): below 6 with at most 3 in a row 176.3-176.9 / 174.9-175.4 ms, below 6 with
 // at most 2 176.3-177.6 / 175.3-175.5, below 4 / 5 / 7 / 8 / 10 179.2-180.1 / 178.4-179.2 /
-// 177.1-178.4 / 177.1-177.9 / 179.0-179.7, against 183.5-184.5 / 181.5-182.3 without.  The
-// plain kernel (1 GPU) does not defer: below 2 / 3 it measured 1073 / 1064 ms against 1048
-// (profiles/r06r_leaf_defer_ab.jsonl), below 4 equal.
+// 177.1-178.4 / 177.1-177.9 / 179.0-179.7, against 183.5-184.5 / 181.5-182.3 without; then
+// at most 4 in a row with the runahead kernel's shading threshold and coop records re-tuned
+// (rt_device.hip RT_SPEC_SHADE_MIN).  The plain kernel (1 GPU) does not defer: below 2 / 3 it
+// measured 1073 / 1064 ms against 1048 (profiles/r06r_leaf_defer_ab.jsonl), below 4 equal.
 #ifndef RT_LEAF_DEFER
 #define RT_LEAF_DEFER 6
 #endif
 #ifndef RT_LEAF_DEFER_MAX
-#define RT_LEAF_DEFER_MAX 3
+#define RT_LEAF_DEFER_MAX 4
 #endif
 constexpr int kLeafDefer = RT_LEAF_DEFER, kLeafDeferMax = RT_LEAF_DEFER_MAX;
 template <bool COUNT, int kCoopLeaves, bool MASK_LOAD, class Stack, class Nodes, class TS, class Hook = NoHook>
