@@ -688,7 +688,13 @@ struct NoHook {
 #define RT_LEAF_DEFER_MAX 4
 #endif
 constexpr int kLeafDefer = RT_LEAF_DEFER, kLeafDeferMax = RT_LEAF_DEFER_MAX;
-template <bool COUNT, int kCoopLeaves, bool MASK_LOAD, class Stack, class Nodes, class TS, class Hook = NoHook>
+// (the plain kernel's threshold, 0: it does not defer; A/B builds only)
+#ifndef RT_PLAIN_LEAF_DEFER
+#define RT_PLAIN_LEAF_DEFER 0
+#endif
+constexpr int kLeafDeferPlain = RT_PLAIN_LEAF_DEFER;
+template <bool COUNT, int kCoopLeaves, bool MASK_LOAD, int DEFER = kLeafDefer, class Stack, class Nodes, class TS,
+          class Hook = NoHook>
 __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r, TS &T, Stack &stk,
                                                const Nodes &nodes, Counters &cnt, bool active, int round_min,
                                                const Hook &hook = Hook{}, int *leaf_defer = nullptr) {
@@ -721,8 +727,8 @@ __device__ __forceinline__ bool trav_step_coop(const DevScene &sc, const Ray &r,
     const int n_leaf = __popcll(lm);
     const int lrank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
     bool skip_leaves = false;   // (wave-uniform)
-    if (kLeafDefer > 0 && leaf_defer) {
-        if (n_leaf > 0 && n_leaf < kLeafDefer && *leaf_defer < kLeafDeferMax && __ballot(at_node) != 0ull) {
+    if (DEFER > 0 && leaf_defer) {
+        if (n_leaf > 0 && n_leaf < DEFER && *leaf_defer < kLeafDeferMax && __ballot(at_node) != 0ull) {
             skip_leaves = true;
             ++*leaf_defer;
         } else {
