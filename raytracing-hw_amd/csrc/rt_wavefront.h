@@ -669,7 +669,7 @@ struct NoHook {
 // kernel takes it and the plain kernel does not.  Two other request shapes were measured and
 // removed: quad-cooperative pair loads with a DPP transpose (1259 ms, 8-way 233 ms) and 36-B
 // triangle loads (1132-1137 ms, 8-way 204 ms: neutral).
-// Leaf deferral (the caller passes `leaf_defer`: the runahead kernel).  A step whose wave has
+// Leaf deferral (both lane-resident kernels pass `leaf_defer`).  A step whose wave has
 // fewer than RT_LEAF_DEFER leaf lanes, and some node lanes, leaves its leaf lanes for the next
 // step (at most RT_LEAF_DEFER_MAX steps in a row), so that the coop step's three triangle
 // loads and its triangle test run for more leaves at once; a leaf lane's triangles, their
@@ -679,8 +679,11 @@ struct NoHook {
 // at most 2 176.3-177.6 / 175.3-175.5, below 4 / 5 / 7 / 8 / 10 179.2-180.1 / 178.4-179.2 /
 // 177.1-178.4 / 177.1-177.9 / 179.0-179.7, against 183.5-184.5 / 181.5-182.3 without; then
 // at most 4 in a row with the runahead kernel's shading threshold and coop records re-tuned
-// (rt_device.hip RT_SPEC_SHADE_MIN).  The plain kernel (1 GPU) does not defer: below 2 / 3 it
-// measured 1073 / 1064 ms against 1048 (profiles/r06r_leaf_defer_ab.jsonl), below 4 equal.
+// (rt_device.hip RT_SPEC_SHADE_MIN).  The plain kernel (1 GPU) defers below 6 as well
+// (RT_PLAIN_LEAF_DEFER): frame 1024.2-1025.3 ms against 1049.1-1051.1, 2-way 567.4-573.3
+// against 572.3-576.6 (three runs each, profiles/r06z_plain_leaf_defer_ab.jsonl; below 8
+// 1030.2-1033.6); below 2 / 3 it measured 1073 / 1064 ms against 1048, below 4 equal
+// (profiles/r06r_leaf_defer_ab.jsonl, with at most 2 deferrals in a row).
 #ifndef RT_LEAF_DEFER
 #define RT_LEAF_DEFER 6
 #endif
@@ -688,9 +691,9 @@ struct NoHook {
 #define RT_LEAF_DEFER_MAX 4
 #endif
 constexpr int kLeafDefer = RT_LEAF_DEFER, kLeafDeferMax = RT_LEAF_DEFER_MAX;
-// (the plain kernel's threshold, 0: it does not defer; A/B builds only)
+// (the plain kernel's threshold; 0: it does not defer)
 #ifndef RT_PLAIN_LEAF_DEFER
-#define RT_PLAIN_LEAF_DEFER 0
+#define RT_PLAIN_LEAF_DEFER 6
 #endif
 constexpr int kLeafDeferPlain = RT_PLAIN_LEAF_DEFER;
 template <bool COUNT, int kCoopLeaves, bool MASK_LOAD, int DEFER = kLeafDefer, class Stack, class Nodes, class TS,
