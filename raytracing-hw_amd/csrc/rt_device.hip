@@ -579,7 +579,7 @@ rt_mega_kernel(DevScene sc_in, ShardGeom g, rtd::WfState st, int spp, float *out
             int leaf_defer = 0;   // (the runahead kernel's leaf steps deferred in a row: rt_wavefront.h RT_LEAF_DEFER)
             do {
                 if (rtd::trav_step_coop<COUNT, kSpec ? kCoopLeavesSpec : kCoopLeavesPlain, kSpec && kSpecMaskLoad,
-                                        kSpec ? rtd::kLeafDefer : rtd::kLeafDeferPlain>(
+                                        kSpec ? rtd::kLeafDefer : (COUNT ? 0 : rtd::kLeafDeferPlain)>(
                         sc, L.r, L.T, S, nodes, cnt, L.state == rtd::M_TRAV, kSpec ? st.round_min : kCoopRoundMinPlain,
                         rtd::NoHook{}, &leaf_defer))
                     L.state = rtd::M_READY;
